@@ -1,0 +1,176 @@
+"""Service configuration: ``APP_*`` environment surface.
+
+Parity with the reference `src/code_interpreter/config.py:18-80`, which uses
+pydantic-settings with ``env_prefix="APP_"`` and ``env_ignore_empty=True``.
+pydantic-settings is not available on the target image, so this is a small
+typed loader with the same observable rules:
+
+* each field ``foo_bar`` is read from ``APP_FOO_BAR`` (case-insensitive);
+* empty values are ignored (the default stays);
+* ``dict``/``list`` fields parse JSON, ``bytes`` fields take the raw UTF-8
+  text (e.g. PEM contents), ``bool`` accepts 1/0/true/false/yes/no/on/off.
+
+Fields below the ``# --- MI355X-native additions`` marker are new; they keep
+the ``APP_`` prefix so a reference deployment's environment still works
+unchanged.
+"""
+
+from __future__ import annotations
+
+import copy
+import dataclasses
+import json
+import os
+import typing
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Mapping, Optional
+
+ENV_PREFIX = "APP_"
+
+
+def default_logging_config() -> Dict[str, Any]:
+    # Same shape/format/levels as the reference (`config.py:22-47`) plus the
+    # loggers this framework adds, so INFO from scheduler/executor is visible.
+    return {
+        "version": 1,
+        "disable_existing_loggers": False,
+        "handlers": {
+            "console": {"class": "logging.StreamHandler", "formatter": "standard"},
+        },
+        "formatters": {
+            "standard": {"format": "[%(levelname)s] [%(request_id)s] %(name)s: %(message)s"},
+        },
+        "root": {"level": "WARNING", "handlers": ["console"], "propagate": True},
+        "loggers": {
+            "kubectl": {"level": "INFO"},
+            "grpc_server": {"level": "INFO"},
+            "code_interpreter_servicer": {"level": "INFO"},
+            "kubernetes_code_executor": {"level": "INFO"},
+            "local_gpu_pool": {"level": "INFO"},
+            "executor_client": {"level": "INFO"},
+        },
+    }
+
+
+@dataclass
+class Config:
+    # logging config: https://docs.python.org/3/library/logging.config.html#logging-config-dictschema
+    logging_config: Dict[str, Any] = field(default_factory=default_logging_config)
+    # address:port of the gRPC server
+    grpc_listen_addr: str = "0.0.0.0:50051"
+    # address:port of the HTTP server
+    http_listen_addr: str = "0.0.0.0:8000"
+    # PEM text of the server certificate / key / CA (TLS only when all three are set)
+    grpc_tls_cert: Optional[bytes] = None
+    grpc_tls_cert_key: Optional[bytes] = None
+    grpc_tls_ca_cert: Optional[bytes] = None
+    # image for executor pods (kubernetes backend)
+    executor_image: str = "localhost/bee-code-executor:local"
+    # 'resources' of the executor container, e.g. {"limits": {"amd.com/gpu": 1}}
+    executor_container_resources: Dict[str, Any] = field(default_factory=dict)
+    # extra fields merged into the executor pod spec (runtimeClassName, volumes, ...)
+    executor_pod_spec_extra: Dict[str, Any] = field(default_factory=dict)
+    # directory of the file-object store
+    file_storage_path: str = "./.tmp/files"
+    # how many executor pods (kubernetes) to keep ready for immediate use
+    executor_pod_queue_target_length: int = 5
+    # prefix of executor pod names; 6 random [a-z0-9] follow
+    executor_pod_name_prefix: str = "code-executor-"
+
+    # --- MI355X-native additions -------------------------------------------
+    # "local" = GPU-pinned sandbox pools on this node (default),
+    # "kubernetes" = reference-style executor pods via kubectl.
+    executor_backend: str = "local"
+    # GPUs to pin executor pools to: None = autodetect, [] = CPU-only pool.
+    gpu_ids: Optional[List[int]] = None
+    # warm single-use sandboxes kept per GPU pool
+    workers_per_gpu_target: int = 4
+    # concurrent executions admitted per GPU pool (others queue)
+    max_inflight_per_gpu: int = 16
+    # per-sandbox HBM quota in bytes (0 = 288 GB / max_inflight_per_gpu minus reserve)
+    hbm_quota_bytes: int = 0
+    # HBM per GPU kept back from quotas (contexts, fragmentation)
+    hbm_reserve_bytes: int = 16 * 1024**3
+    # total HBM per GPU used for quota accounting (MI355X: 288 GB)
+    hbm_total_bytes: int = 288 * 1000**3
+    # default execution timeout in seconds (reference: 60 s, `server.rs:201`)
+    default_timeout: float = 60.0
+    # where sandboxes (workspace + runtime-packages + logs) are created
+    sandbox_root: str = "./.tmp/sandboxes"
+    # path of the native executor daemon binary (None = in-tree build)
+    executor_binary: Optional[str] = None
+    # python interpreter used for sandbox zygotes
+    worker_python: Optional[str] = None
+    # initialise HIP + load the kernel library while a sandbox waits in the pool
+    worker_warm_gpu: bool = True
+    # report changed files recursively (reference: top level only, `server.rs:117-137`)
+    changed_files_recursive: bool = False
+    # local wheelhouse used for auto-installing missing imports (offline pip)
+    wheelhouse: Optional[str] = None
+    # fault injection: probability that spawning a sandbox fails (tests)
+    fault_spawn_fail_rate: float = 0.0
+    # max bytes of stdout / stderr returned per execution
+    max_output_bytes: int = 16 * 1024 * 1024
+
+    def __init__(self, _env: Optional[Mapping[str, str]] = None, **overrides: Any) -> None:
+        env = os.environ if _env is None else _env
+        lowered = {k.lower(): v for k, v in env.items() if k.upper().startswith(ENV_PREFIX)}
+        hints = typing.get_type_hints(type(self))
+        for f in dataclasses.fields(self):
+            if f.name in overrides:
+                value = overrides.pop(f.name)
+            else:
+                raw = lowered.get((ENV_PREFIX + f.name).lower())
+                if raw is not None and raw != "":
+                    value = _coerce(f.name, raw, hints[f.name])
+                elif f.default is not dataclasses.MISSING:
+                    value = copy.deepcopy(f.default)
+                else:
+                    value = f.default_factory()  # type: ignore[misc]
+            setattr(self, f.name, value)
+        if overrides:
+            raise TypeError(f"unknown config fields: {sorted(overrides)}")
+
+    def as_dict(self) -> Dict[str, Any]:
+        return {f.name: getattr(self, f.name) for f in dataclasses.fields(self)}
+
+
+_TRUE = {"1", "true", "yes", "on", "y", "t"}
+_FALSE = {"0", "false", "no", "off", "n", "f"}
+
+
+def _coerce(name: str, raw: str, hint: Any) -> Any:
+    origin = typing.get_origin(hint)
+    args = typing.get_args(hint)
+    if origin is typing.Union:  # Optional[X]
+        inner = [a for a in args if a is not type(None)]
+        if raw.strip().lower() in ("null", "none"):
+            return None
+        return _coerce(name, raw, inner[0])
+    try:
+        if hint is bytes:
+            return raw.encode("utf-8")
+        if hint is str:
+            return raw
+        if hint is bool:
+            low = raw.strip().lower()
+            if low in _TRUE:
+                return True
+            if low in _FALSE:
+                return False
+            raise ValueError(raw)
+        if hint is int:
+            return int(raw.strip())
+        if hint is float:
+            return float(raw.strip())
+        if origin in (dict, list) or hint in (dict, list):
+            value = json.loads(raw)
+            expected = origin or hint
+            if not isinstance(value, expected):
+                raise ValueError(f"expected JSON {expected.__name__}")
+            if origin is list and args and args[0] is int:
+                value = [int(v) for v in value]
+            return value
+    except (ValueError, json.JSONDecodeError) as e:
+        raise ValueError(f"invalid value for {ENV_PREFIX}{name.upper()}: {raw!r} ({e})") from e
+    raise TypeError(f"unsupported config type for {name}: {hint!r}")

@@ -1,0 +1,687 @@
+"""``DeviceArray``: a minimal numpy-like array in MI355X HBM, driven by the
+hand-written beekern kernels.
+
+Sandboxed user code calls these in place of numpy (BASELINE.json north
+star).  The benchmark payload `examples/benchmark-numpy.py:18-22` becomes::
+
+    import beekern as bk
+    x = bk.random.rand(10**8)          # Philox kernel, f64, stays in HBM
+    result = bk.sum(bk.square(x))      # fused square+sum: one HBM read pass
+
+``square`` (and ``x * x`` / ``x ** 2``) returns a *lazy* array: if the only
+consumer is a reduction the square is fused into it (no 800 MB temporary);
+any other use materialises it with the elementwise kernel.  All kernels are
+enqueued on one stream (the HIP null stream, which torch's default stream
+also orders against), so torch tensors and DeviceArrays interleave safely.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import threading
+from typing import Any, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from . import _native
+from ._native import DTYPE_CODES, DTYPE_SIZES, BeekernError, check
+
+Shape = Tuple[int, ...]
+
+_UNARY = {
+    "square": 0, "abs": 1, "negative": 2, "sqrt": 3, "exp": 4, "log": 5, "relu": 6,
+    "sin": 7, "cos": 8, "tanh": 9, "sigmoid": 10, "copy": 11,
+}
+_BINARY = {"add": 0, "subtract": 1, "multiply": 2, "divide": 3, "maximum": 4, "minimum": 5, "power": 6}
+_REDUCE = {"sum": 0, "square_sum": 1, "abs_sum": 2, "max": 3, "min": 4, "dot": 5}
+_SUPPORTED = ("float32", "float64", "bfloat16")
+
+_NP_DTYPES = {"float32": np.float32, "float64": np.float64}
+
+_state_lock = threading.Lock()
+_initialized_device: Optional[int] = None
+_stream = ctypes.c_void_p(0)  # HIP null stream
+_workspace: Optional["_Buffer"] = None
+_scalar_out: Optional["_Buffer"] = None
+
+
+def normalize_dtype(dtype: Any) -> str:
+    if dtype is None:
+        return "float64"
+    if isinstance(dtype, str):
+        name = {"bf16": "bfloat16", "f32": "float32", "f64": "float64", "double": "float64", "float": "float64"}.get(
+            dtype, dtype
+        )
+    else:
+        name = str(getattr(dtype, "name", None) or np.dtype(dtype).name)
+        name = name.replace("torch.", "")
+    if name not in _SUPPORTED:
+        raise TypeError(f"unsupported dtype {dtype!r}; beekern supports {_SUPPORTED}")
+    return name
+
+
+def init(device: Optional[int] = None) -> int:
+    """Initialise HIP on ``device`` (default: 0 of the visible set) and load
+    the kernels; idempotent.  Sandboxes call this while waiting in the warm
+    pool so user code never pays it."""
+    global _initialized_device, _workspace, _scalar_out
+    if _initialized_device is not None:
+        return _initialized_device
+    with _state_lock:
+        if _initialized_device is None:
+            dev = int(os.environ.get("BEE_DEVICE", "0")) if device is None else int(device)
+            check(_native.lib().bk_init(dev), "bk_init")
+            _initialized_device = dev
+            _workspace = _Buffer(_native.lib().bk_reduce_workspace_bytes())
+            _scalar_out = _Buffer(256)
+    return _initialized_device  # type: ignore[return-value]
+
+
+def is_initialized() -> bool:
+    return _initialized_device is not None
+
+
+def synchronize() -> None:
+    if is_initialized():
+        check(_native.lib().bk_sync(_stream), "bk_sync")
+
+
+def memory_stats() -> dict:
+    stats = (ctypes.c_int64 * 4)()
+    check(_native.lib().bk_memory_stats(stats), "bk_memory_stats")
+    return {"in_use": stats[0], "cached": stats[1], "peak": stats[2], "quota": stats[3]}
+
+
+def set_quota(nbytes: int) -> None:
+    check(_native.lib().bk_set_quota(int(nbytes)), "bk_set_quota")
+
+
+def empty_cache() -> None:
+    check(_native.lib().bk_empty_cache(), "bk_empty_cache")
+
+
+def device_info() -> dict:
+    init()
+    info = (ctypes.c_int64 * 5)()
+    name = ctypes.create_string_buffer(64)
+    check(_native.lib().bk_device_info(info, name, 64), "bk_device_info")
+    return {
+        "arch": name.value.decode(),
+        "compute_units": info[0],
+        "total_bytes": info[1],
+        "free_bytes": info[2],
+        "clock_khz": info[3],
+        "lds_bytes_per_cu": info[4],
+    }
+
+
+class _Buffer:
+    """Owns one device allocation from the caching, quota-checked allocator."""
+
+    __slots__ = ("ptr", "nbytes", "_owner", "__weakref__")
+
+    def __init__(self, nbytes: int, ptr: Optional[int] = None, owner: Any = None) -> None:
+        self.nbytes = int(nbytes)
+        self._owner = owner
+        if ptr is not None:
+            self.ptr = int(ptr)
+            return
+        init()
+        out = ctypes.c_void_p()
+        check(_native.lib().bk_malloc(ctypes.byref(out), max(self.nbytes, 1)), "bk_malloc")
+        self.ptr = int(out.value or 0)
+
+    def __del__(self) -> None:
+        if self._owner is None and getattr(self, "ptr", 0) and _native.is_loaded():
+            try:
+                _native.lib().bk_free(ctypes.c_void_p(self.ptr))
+            except Exception:
+                pass
+
+
+class DeviceArray:
+    """Contiguous row-major array in device memory (or a lazy unary view)."""
+
+    __array_priority__ = 1000
+
+    def __init__(self, shape: Sequence[int], dtype: str, buffer: Optional[_Buffer] = None, lazy=None, strides_t=False):
+        self.shape: Shape = tuple(int(s) for s in shape)
+        self.dtype = normalize_dtype(dtype)
+        self._lazy = lazy  # ("square", src) until materialised
+        self._transposed = strides_t  # 2-D transposed view of a contiguous buffer
+        if buffer is None and lazy is None:
+            buffer = _Buffer(self.nbytes)
+        self._buf = buffer
+
+    # ---- basic properties ----------------------------------------------------
+    @property
+    def size(self) -> int:
+        return int(math.prod(self.shape)) if self.shape else 1
+
+    @property
+    def ndim(self) -> int:
+        return len(self.shape)
+
+    @property
+    def itemsize(self) -> int:
+        return DTYPE_SIZES[self.dtype]
+
+    @property
+    def nbytes(self) -> int:
+        return self.size * self.itemsize
+
+    @property
+    def ptr(self) -> int:
+        self._materialize()
+        return self._buf.ptr  # type: ignore[union-attr]
+
+    def __len__(self) -> int:
+        if not self.shape:
+            raise TypeError("len() of a 0-d array")
+        return self.shape[0]
+
+    def __repr__(self) -> str:
+        kind = "lazy " if self._lazy else ""
+        return f"DeviceArray({kind}shape={self.shape}, dtype={self.dtype})"
+
+    # ---- lazy fusion ------------------------------------------------------------
+    def _materialize(self) -> "DeviceArray":
+        if self._lazy is not None:
+            op, src = self._lazy
+            self._buf = _Buffer(self.nbytes)
+            check(
+                _native.lib().bk_unary(_UNARY[op], DTYPE_CODES[self.dtype], _vp(src.ptr), _vp(self._buf.ptr), self.size, _stream),
+                f"bk_unary({op})",
+            )
+            self._lazy = None
+        if self._transposed:
+            src = self._buf
+            rows, cols = self.shape[1], self.shape[0]  # underlying buffer is (rows, cols)
+            out = _Buffer(self.nbytes)
+            if self.dtype == "bfloat16":
+                check(_native.lib().bk_transpose_bf16(_vp(src.ptr), _vp(out.ptr), rows, cols, cols, rows, _stream), "transpose")
+            else:
+                host = _download(src, (rows, cols), self.dtype)
+                out = _upload(np.ascontiguousarray(host.T), self.dtype)
+            self._buf = out
+            self._transposed = False
+        return self
+
+    # ---- host transfer ------------------------------------------------------------
+    def numpy(self) -> np.ndarray:
+        self._materialize()
+        return _download(self._buf, self.shape, self.dtype)
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.numpy()
+        return a.astype(dtype) if dtype is not None else a
+
+    def tolist(self):
+        return self.numpy().tolist()
+
+    def item(self):
+        if self.size != 1:
+            raise ValueError("item() needs a size-1 array")
+        return self.numpy().reshape(()).item()
+
+    def __float__(self) -> float:
+        return float(self.item())
+
+    # ---- shape ---------------------------------------------------------------------
+    def reshape(self, *shape) -> "DeviceArray":
+        if len(shape) == 1 and isinstance(shape[0], (tuple, list)):
+            shape = tuple(shape[0])
+        shape = list(shape)
+        if -1 in shape:
+            known = math.prod(s for s in shape if s != -1)
+            shape[shape.index(-1)] = self.size // max(known, 1)
+        if math.prod(shape) != self.size:
+            raise ValueError(f"cannot reshape {self.shape} to {tuple(shape)}")
+        self._materialize()
+        return DeviceArray(shape, self.dtype, buffer=self._buf)
+
+    @property
+    def T(self) -> "DeviceArray":
+        if self.ndim != 2:
+            raise ValueError("T needs a 2-D array")
+        self._materialize()
+        return DeviceArray((self.shape[1], self.shape[0]), self.dtype, buffer=self._buf, strides_t=True)
+
+    def astype(self, dtype) -> "DeviceArray":
+        dt = normalize_dtype(dtype)
+        if dt == self.dtype:
+            return self.copy()
+        self._materialize()
+        out = DeviceArray(self.shape, dt)
+        check(
+            _native.lib().bk_cast(DTYPE_CODES[self.dtype], DTYPE_CODES[dt], _vp(self.ptr), _vp(out.ptr), self.size, _stream),
+            "bk_cast",
+        )
+        return out
+
+    def copy(self) -> "DeviceArray":
+        return _unary("copy", self)
+
+    # ---- reductions ----------------------------------------------------------------
+    def sum(self):
+        return sum(self)
+
+    def mean(self):
+        return sum(self) / self.size
+
+    def max(self):
+        return _reduce("max", self)
+
+    def min(self):
+        return _reduce("min", self)
+
+    # ---- operators -----------------------------------------------------------------
+    def __add__(self, o): return _binary("add", self, o)
+    def __radd__(self, o): return _binary("add", self, o)
+    def __sub__(self, o): return _binary("subtract", self, o)
+    def __rsub__(self, o): return _binary("subtract", self, o, reversed_=True)
+    def __mul__(self, o):
+        if o is self:
+            return square(self)
+        return _binary("multiply", self, o)
+    def __rmul__(self, o): return _binary("multiply", self, o)
+    def __truediv__(self, o): return _binary("divide", self, o)
+    def __rtruediv__(self, o): return _binary("divide", self, o, reversed_=True)
+    def __pow__(self, o):
+        if isinstance(o, (int, float)) and o == 2:
+            return square(self)
+        return _binary("power", self, o)
+    def __neg__(self): return _unary("negative", self)
+    def __abs__(self): return _unary("abs", self)
+    def __matmul__(self, o): return matmul(self, o)
+
+
+def _vp(p: int) -> ctypes.c_void_p:
+    return ctypes.c_void_p(p)
+
+
+def _np_view_dtype(dtype: str):
+    return np.uint16 if dtype == "bfloat16" else _NP_DTYPES[dtype]
+
+
+def _download(buf: _Buffer, shape: Shape, dtype: str) -> np.ndarray:
+    host = np.empty(shape, dtype=_np_view_dtype(dtype))
+    if host.nbytes:
+        check(_native.lib().bk_memcpy(host.ctypes.data, _vp(buf.ptr), host.nbytes, 2, _stream), "download")
+    if dtype == "bfloat16":
+        return (host.astype(np.uint32) << 16).view(np.float32)
+    return host
+
+
+def _upload(host: np.ndarray, dtype: str) -> _Buffer:
+    host = np.ascontiguousarray(host)
+    buf = _Buffer(host.nbytes)
+    if host.nbytes:
+        check(_native.lib().bk_memcpy(_vp(buf.ptr), host.ctypes.data, host.nbytes, 1, _stream), "upload")
+    return buf
+
+
+def _f32_to_bf16_bits(a: np.ndarray) -> np.ndarray:
+    u = np.ascontiguousarray(a, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    rounded = (u + 0x7FFF + ((u >> 16) & 1)) >> 16
+    out = rounded.astype(np.uint16)
+    nan = np.isnan(a)
+    if nan.any():
+        out[nan] = 0x7FC0
+    return out
+
+
+# ---- constructors -------------------------------------------------------------------
+
+def empty(shape, dtype="float64") -> DeviceArray:
+    shape = (shape,) if isinstance(shape, int) else tuple(shape)
+    return DeviceArray(shape, dtype)
+
+
+def full(shape, value: float, dtype="float64") -> DeviceArray:
+    a = empty(shape, dtype)
+    dt = a.dtype
+    if dt == "float64":
+        pattern, width = int(np.array(value, np.float64).view(np.uint64)), 8
+    elif dt == "float32":
+        pattern, width = int(np.array(value, np.float32).view(np.uint32)), 4
+    else:
+        pattern, width = int(_f32_to_bf16_bits(np.array([value], np.float32))[0]), 2
+    check(_native.lib().bk_fill(_vp(a.ptr), a.nbytes, pattern, width, _stream), "bk_fill")
+    return a
+
+
+def zeros(shape, dtype="float64") -> DeviceArray:
+    return full(shape, 0.0, dtype)
+
+
+def ones(shape, dtype="float64") -> DeviceArray:
+    return full(shape, 1.0, dtype)
+
+
+def asarray(obj, dtype=None) -> DeviceArray:
+    if isinstance(obj, DeviceArray):
+        return obj if dtype is None or normalize_dtype(dtype) == obj.dtype else obj.astype(dtype)
+    if _is_torch_tensor(obj):
+        return from_torch(obj) if dtype is None else from_torch(obj).astype(dtype)
+    host = np.asarray(obj)
+    dt = normalize_dtype(dtype if dtype is not None else (host.dtype if host.dtype.kind == "f" else "float64"))
+    if dt == "bfloat16":
+        buf = _upload(_f32_to_bf16_bits(host.astype(np.float32)), "bfloat16")
+    else:
+        buf = _upload(host.astype(_NP_DTYPES[dt], copy=False), dt)
+    return DeviceArray(host.shape, dt, buffer=buf)
+
+
+from_numpy = asarray
+array = asarray
+
+
+def _is_torch_tensor(x) -> bool:
+    t = type(x)
+    return t.__module__.startswith("torch") and t.__name__ in ("Tensor", "Parameter")
+
+
+def from_torch(t) -> DeviceArray:
+    """Zero-copy view of a contiguous HIP torch tensor (keeps it alive)."""
+    if not t.is_cuda:
+        return asarray(t.numpy())
+    t = t.contiguous()
+    dt = normalize_dtype(str(t.dtype).replace("torch.", ""))
+    init()
+    return DeviceArray(tuple(t.shape), dt, buffer=_Buffer(t.numel() * t.element_size(), ptr=t.data_ptr(), owner=t))
+
+
+def to_torch(a: DeviceArray):
+    import torch
+
+    host = a.numpy()
+    dt = {"float32": torch.float32, "float64": torch.float64, "bfloat16": torch.bfloat16}[a.dtype]
+    return torch.from_numpy(host).to(device="cuda", dtype=dt)
+
+
+# ---- elementwise / reductions ------------------------------------------------------
+
+def _as_operand(x) -> DeviceArray:
+    if isinstance(x, DeviceArray):
+        return x
+    return asarray(x)
+
+
+def _unary(op: str, x) -> DeviceArray:
+    x = _as_operand(x)._materialize()
+    out = DeviceArray(x.shape, x.dtype)
+    check(_native.lib().bk_unary(_UNARY[op], DTYPE_CODES[x.dtype], _vp(x.ptr), _vp(out.ptr), x.size, _stream), f"bk_unary({op})")
+    return out
+
+
+def square(x) -> DeviceArray:
+    """Lazy x**2: fused into a following reduction, else materialised."""
+    x = _as_operand(x)._materialize()
+    return DeviceArray(x.shape, x.dtype, lazy=("square", x))
+
+
+def _binary(op: str, a, b, reversed_: bool = False) -> DeviceArray:
+    a = _as_operand(a)._materialize()
+    if isinstance(b, (int, float, np.floating, np.integer)):
+        out = DeviceArray(a.shape, a.dtype)
+        mode = 2 if reversed_ else 1
+        check(
+            _native.lib().bk_binary(_BINARY[op], DTYPE_CODES[a.dtype], mode, _vp(a.ptr), None, float(b), _vp(out.ptr), a.size, _stream),
+            f"bk_binary({op})",
+        )
+        return out
+    b = _as_operand(b)._materialize()
+    if b.shape != a.shape or b.dtype != a.dtype:
+        if b.size == 1:
+            return _binary(op, a, float(b.item()), reversed_)
+        raise ValueError(f"beekern {op}: shapes/dtypes must match ({a.shape} {a.dtype} vs {b.shape} {b.dtype})")
+    if reversed_:
+        a, b = b, a
+    out = DeviceArray(a.shape, a.dtype)
+    check(
+        _native.lib().bk_binary(_BINARY[op], DTYPE_CODES[a.dtype], 0, _vp(a.ptr), _vp(b.ptr), 0.0, _vp(out.ptr), a.size, _stream),
+        f"bk_binary({op})",
+    )
+    return out
+
+
+def _reduce(op: str, x: DeviceArray, y: Optional[DeviceArray] = None) -> np.float64:
+    init()
+    lib = _native.lib()
+    b_ptr = _vp(y.ptr) if y is not None else None
+    check(
+        lib.bk_reduce(_REDUCE[op], DTYPE_CODES[x.dtype], _vp(x.ptr), b_ptr, x.size, _vp(_workspace.ptr), _vp(_scalar_out.ptr), _stream),
+        f"bk_reduce({op})",
+    )
+    out = np.zeros(1, np.float64)
+    check(lib.bk_memcpy(out.ctypes.data, _vp(_scalar_out.ptr), 8, 2, _stream), "reduce readback")
+    return np.float64(out[0])
+
+
+def sum(x) -> np.float64:  # noqa: A001 - numpy-compatible name
+    x = _as_operand(x)
+    if x._lazy is not None and x._lazy[0] == "square":
+        return _reduce("square_sum", x._lazy[1])  # fused: x never materialised
+    return _reduce("sum", x._materialize())
+
+
+def square_sum(x) -> np.float64:
+    return _reduce("square_sum", _as_operand(x)._materialize())
+
+
+def mean(x) -> np.float64:
+    x = _as_operand(x)
+    return sum(x) / x.size
+
+
+def dot(a, b) -> np.float64:
+    a, b = _as_operand(a)._materialize(), _as_operand(b)._materialize()
+    if a.ndim == 2 or b.ndim == 2:
+        return matmul(a, b)
+    if a.shape != b.shape or a.dtype != b.dtype:
+        raise ValueError("dot: 1-D operands must match in shape and dtype")
+    return _reduce("dot", a, b)
+
+
+def amax(x): return _reduce("max", _as_operand(x)._materialize())
+def amin(x): return _reduce("min", _as_operand(x)._materialize())
+
+
+def _make_unary(name):
+    def fn(x):
+        return _unary(name, x)
+    fn.__name__ = name
+    return fn
+
+
+abs = _make_unary("abs")  # noqa: A001
+negative = _make_unary("negative")
+sqrt = _make_unary("sqrt")
+exp = _make_unary("exp")
+log = _make_unary("log")
+relu = _make_unary("relu")
+sin = _make_unary("sin")
+cos = _make_unary("cos")
+tanh = _make_unary("tanh")
+sigmoid = _make_unary("sigmoid")
+
+
+def add(a, b): return _binary("add", a, b)
+def subtract(a, b): return _binary("subtract", a, b)
+def multiply(a, b): return _binary("multiply", a, b)
+def divide(a, b): return _binary("divide", a, b)
+def maximum(a, b): return _binary("maximum", a, b)
+def minimum(a, b): return _binary("minimum", a, b)
+def power(a, b): return _binary("power", a, b)
+
+
+# ---- matmul --------------------------------------------------------------------------
+
+def matmul(a, b, out_dtype: str = "bfloat16") -> DeviceArray:
+    """C = A @ B on the bf16 MFMA GEMM (f32 accumulate).
+
+    Operands are converted to bf16 if needed; ``b`` is consumed as Bt[N, K]
+    (K-contiguous), so a plain row-major ``b`` is transposed once on device
+    (~1 % of a 4096³ GEMM) and ``b.T`` views are used directly.
+    """
+    a = _as_operand(a)
+    b = _as_operand(b)
+    if a.ndim != 2 or b.ndim != 2 or a.shape[1] != b.shape[0]:
+        raise ValueError(f"matmul: incompatible shapes {a.shape} @ {b.shape}")
+    M, K = a.shape
+    N = b.shape[1]
+    if a.dtype != "bfloat16":
+        a = a.astype("bfloat16")
+    a._materialize()
+    if b._transposed and b.dtype == "bfloat16" and b._lazy is None:
+        bt_buf = b._buf  # underlying buffer already is Bt[N, K]
+    else:
+        if b.dtype != "bfloat16":
+            b = b.astype("bfloat16")
+        b._materialize()
+        bt = DeviceArray((N, K), "bfloat16")
+        check(_native.lib().bk_transpose_bf16(_vp(b.ptr), _vp(bt.ptr), K, N, N, K, _stream), "transpose")
+        bt_buf = bt._buf
+        b = bt
+    out_dtype = normalize_dtype(out_dtype)
+    c = DeviceArray((M, N), out_dtype)
+    check(
+        _native.lib().bk_gemm_bf16_tn(
+            _vp(a.ptr), _vp(bt_buf.ptr), _vp(c.ptr), M, N, K, K, K, N, 1.0, 0.0, DTYPE_CODES[out_dtype], _stream
+        ),
+        "bk_gemm_bf16_tn",
+    )
+    return c
+
+
+def gemm_bf16_tn(a: DeviceArray, bt: DeviceArray, out_dtype: str = "bfloat16", alpha: float = 1.0) -> DeviceArray:
+    """Raw C = alpha * A . Bt^T with both operands already bf16 [M,K] / [N,K]."""
+    M, K = a.shape
+    N = bt.shape[0]
+    c = DeviceArray((M, N), out_dtype)
+    check(
+        _native.lib().bk_gemm_bf16_tn(
+            _vp(a.ptr), _vp(bt.ptr), _vp(c.ptr), M, N, K, K, K, N, float(alpha), 0.0, DTYPE_CODES[normalize_dtype(out_dtype)], _stream
+        ),
+        "bk_gemm_bf16_tn",
+    )
+    return c
+
+
+# ---- random ----------------------------------------------------------------------------
+
+class Generator:
+    """Counter-based Philox4x32-10 stream on the device (numpy.random subset)."""
+
+    def __init__(self, seed: Optional[int] = None) -> None:
+        self.seed(seed)
+
+    def seed(self, seed: Optional[int] = None) -> None:
+        if seed is None:
+            seed = int.from_bytes(os.urandom(8), "little")
+        self._seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self._offset = 0
+
+    def _advance(self, n: int, per_call: int) -> int:
+        off = self._offset
+        self._offset += (n + per_call - 1) // per_call
+        return off
+
+    def random(self, size=None, dtype="float64") -> DeviceArray:
+        return self.uniform(0.0, 1.0, size, dtype)
+
+    def rand(self, *shape, dtype="float64") -> DeviceArray:
+        return self.uniform(0.0, 1.0, shape or (1,), dtype)
+
+    def uniform(self, low=0.0, high=1.0, size=None, dtype="float64") -> DeviceArray:
+        shape = _shape_of(size)
+        out = DeviceArray(shape, dtype)
+        per = 2 if out.dtype == "float64" else 4
+        if out.dtype == "bfloat16":
+            tmp = self.uniform(low, high, shape, "float32")
+            return tmp.astype("bfloat16")
+        check(
+            _native.lib().bk_rand_uniform(
+                _vp(out.ptr), out.size, DTYPE_CODES[out.dtype], self._seed, self._advance(out.size, per), float(low), float(high), _stream
+            ),
+            "bk_rand_uniform",
+        )
+        return out
+
+    def randn(self, *shape, dtype="float64") -> DeviceArray:
+        return self.normal(0.0, 1.0, shape or (1,), dtype)
+
+    def standard_normal(self, size=None, dtype="float64") -> DeviceArray:
+        return self.normal(0.0, 1.0, size, dtype)
+
+    def normal(self, loc=0.0, scale=1.0, size=None, dtype="float64") -> DeviceArray:
+        shape = _shape_of(size)
+        out = DeviceArray(shape, dtype)
+        if out.dtype == "bfloat16":
+            return self.normal(loc, scale, shape, "float32").astype("bfloat16")
+        per = 2 if out.dtype == "float64" else 4
+        check(
+            _native.lib().bk_rand_normal(
+                _vp(out.ptr), out.size, DTYPE_CODES[out.dtype], self._seed, self._advance(out.size, per), float(loc), float(scale), _stream
+            ),
+            "bk_rand_normal",
+        )
+        return out
+
+
+def _shape_of(size) -> Shape:
+    if size is None:
+        return (1,)
+    if isinstance(size, (int, np.integer)):
+        return (int(size),)
+    if len(size) == 1 and isinstance(size[0], (tuple, list)):
+        return tuple(int(s) for s in size[0])
+    return tuple(int(s) for s in size)
+
+
+class _RandomModule:
+    """``bk.random`` — module-level functions on a default generator."""
+
+    def __init__(self) -> None:
+        self._gen: Optional[Generator] = None
+
+    @property
+    def gen(self) -> Generator:
+        if self._gen is None:
+            self._gen = Generator()
+        return self._gen
+
+    def seed(self, seed=None): self.gen.seed(seed)
+    def default_rng(self, seed=None) -> Generator: return Generator(seed)
+    def rand(self, *shape, dtype="float64"): return self.gen.rand(*shape, dtype=dtype)
+    def randn(self, *shape, dtype="float64"): return self.gen.randn(*shape, dtype=dtype)
+    def random(self, size=None, dtype="float64"): return self.gen.random(size, dtype)
+    def uniform(self, low=0.0, high=1.0, size=None, dtype="float64"): return self.gen.uniform(low, high, size, dtype)
+    def normal(self, loc=0.0, scale=1.0, size=None, dtype="float64"): return self.gen.normal(loc, scale, size, dtype)
+    def standard_normal(self, size=None, dtype="float64"): return self.gen.standard_normal(size, dtype)
+
+
+random = _RandomModule()
+
+
+class Timer:
+    """Device-side timing with HIP events: ``with Timer() as t: ...; t.ms``."""
+
+    def __enter__(self):
+        init()
+        s, e = ctypes.c_void_p(), ctypes.c_void_p()
+        check(_native.lib().bk_event_pair_create(ctypes.byref(s), ctypes.byref(e)), "events")
+        self._s, self._e = s, e
+        check(_native.lib().bk_event_record(s, _stream), "event record")
+        return self
+
+    def __exit__(self, *exc):
+        lib = _native.lib()
+        check(lib.bk_event_record(self._e, _stream), "event record")
+        self.ms = float(lib.bk_event_elapsed_ms(self._s, self._e))
+        lib.bk_event_destroy(self._s)
+        lib.bk_event_destroy(self._e)
+        return False

@@ -1,0 +1,289 @@
+// bf16 GEMM on gfx950 matrix cores: C[M,N] = alpha * A[M,K] . Bt[N,K]^T
+// (+ beta * C), f32 accumulation, bf16 or f32 output.
+//
+// Fast path (M%128 == N%128 == K%64 == 0, 16-B aligned rows): 128x128x64
+// block tile, 256 threads = 4 waves in 2x2, each wave a 64x64 sub-tile of
+// 4x4 `v_mfma_f32_16x16x32_bf16` accumulators (64 AGPR/VGPR).  Operands go
+// HBM -> LDS with `global_load_lds_dwordx4` (one wave-instruction = 1 KiB =
+// 8 tile rows; no VGPR staging), two LDS buffers so tile t+1 streams in while
+// tile t is multiplied.  The LDS image is lane-linear (a DMA constraint), so
+// the bank-conflict XOR swizzle is applied to the per-lane GLOBAL source
+// address and undone on the ds_read_b128 address (cdna_hip_programming §5.4
+// rule 21): 16-B chunk c of row r lives at chunk c ^ ((r >> 1) & 7), which
+// makes every 16-lane ds_read_b128 group conflict-free for the MFMA fragment
+// pattern (16 rows x one chunk).  Block ids are remapped XCD-aware and
+// grouped along M so the 8 private L2s each see a compact panel of A and B.
+//
+// Generic path: any shape / alignment, 64x64x32 tile, guarded register
+// staging with zero fill.  Same MFMA and fragment maps, slower.
+#include "bk_common.hpp"
+
+namespace bk {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef const __attribute__((address_space(1))) void* global_void_ptr;
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int kGemmThreads = 256;
+constexpr int kRowBytes = BK * 2;                       // 128 B per tile row
+constexpr int kTileElems = (BM + BN) * BK;              // A + B per stage
+constexpr int kGroupM = 8;
+
+// bijective XCD remap: blocks b, b+8, b+16.. share an XCD under round-robin
+// dispatch; give each XCD a contiguous range of logical tiles.
+__device__ __forceinline__ int xcd_remap(int b, int nblocks) {
+  const int xcd = b % kNumXCD, q = nblocks / kNumXCD, r = nblocks % kNumXCD;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + b / kNumXCD;
+}
+
+__device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+// Stage one BMxBK (or BNxBK) tile: 16 wave-instructions per operand, 4 per
+// wave.  Lane l of instruction i writes LDS bytes [l*16, l*16+16) of rows
+// 8i..8i+7, i.e. row 8i + (l>>3), physical chunk l&7, fetched from the
+// logical chunk that maps there.
+__device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ g, int ld, int row0, int k0,
+                                           uint16_t* lds_tile, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ins = wave * 4 + i;          // 0..15
+    const int r = ins * 8 + (lane >> 3);   // tile row
+    const int pc = lane & 7;               // physical chunk in LDS
+    const int c = swz_chunk(r, pc);        // logical chunk (involution)
+    const uint16_t* src = g + (int64_t)(row0 + r) * ld + k0 + c * 8;
+    uint16_t* dst = lds_tile + ins * 8 * BK;  // wave-uniform base
+    __builtin_amdgcn_global_load_lds((global_void_ptr)src, (lds_void_ptr)dst, 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 read_frag(const uint16_t* lds_tile, int row, int chunk) {
+  const int pc = swz_chunk(row, chunk);
+  return *reinterpret_cast<const bf16x8*>(lds_tile + row * BK + pc * 8);
+}
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_fast(const uint16_t* __restrict__ A,
+                                                                     const uint16_t* __restrict__ Bt,
+                                                                     void* __restrict__ C, int M, int N, int K,
+                                                                     int lda, int ldb, int ldc, float alpha,
+                                                                     float beta) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * kTileElems];  // 64 KiB
+
+  const int nbm = M / BM, nbn = N / BN, nblocks = nbm * nbn;
+  int b = xcd_remap(blockIdx.x, nblocks);
+  // grouped ordering along M for L2 reuse of the B panel
+  const int group = kGroupM * nbn;
+  const int first_m = (b / group) * kGroupM;
+  const int gm = min(nbm - first_m, kGroupM);
+  const int tm = first_m + (b % group) % gm;
+  const int tn = (b % group) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;  // 2x2 waves, 64x64 each
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  stage_tile(A, lda, m0, 0, smem, wave, lane);
+  stage_tile(Bt, ldb, n0, 0, smem + BM * BK, wave, lane);
+  __syncthreads();  // vmcnt(0) + barrier: tile 0 resident
+
+  for (int t = 0; t < nk; ++t) {
+    uint16_t* cur = smem + (t & 1) * kTileElems;
+    if (t + 1 < nk) {  // prefetch next K tile into the other buffer
+      uint16_t* nxt = smem + ((t + 1) & 1) * kTileElems;
+      stage_tile(A, lda, m0, (t + 1) * BK, nxt, wave, lane);
+      stage_tile(Bt, ldb, n0, (t + 1) * BK, nxt + BM * BK, wave, lane);
+    }
+    const uint16_t* tA = cur;
+    const uint16_t* tB = cur + BM * BK;
+#pragma unroll
+    for (int s = 0; s < BK / 32; ++s) {
+      const int chunk = s * 4 + (lane >> 4);
+      bf16x8 af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag(tA, wm * 64 + i * 16 + (lane & 15), chunk);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = read_frag(tB, wn * 64 + j * 16 + (lane & 15), chunk);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();  // next tile landed (vmcnt(0)) and every wave done reading `cur`
+  }
+
+  // epilogue: 16x16 C/D map: col = lane & 15, row = (lane >> 4) * 4 + reg
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const int col = n0 + wn * 64 + j * 16 + (lane & 15);
+        float v = alpha * acc[i][j][r];
+        if constexpr (OUT_BF16) {
+          uint16_t* c = (uint16_t*)C + (int64_t)row * ldc + col;
+          if (beta != 0.f) v += beta * bf16_bits_to_float(*c);
+          *c = float_to_bf16_bits(v);
+        } else {
+          float* c = (float*)C + (int64_t)row * ldc + col;
+          if (beta != 0.f) v += beta * *c;
+          *c = v;
+        }
+      }
+}
+
+// ---- generic path ------------------------------------------------------------
+constexpr int GBM = 64, GBN = 64, GBK = 32;
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(256) void gemm_bf16_tn_generic(const uint16_t* __restrict__ A,
+                                                            const uint16_t* __restrict__ Bt, void* __restrict__ C,
+                                                            int M, int N, int K, int lda, int ldb, int ldc,
+                                                            float alpha, float beta) {
+  __shared__ __attribute__((aligned(16))) uint16_t sA[GBM * (GBK + 8)];
+  __shared__ __attribute__((aligned(16))) uint16_t sB[GBN * (GBK + 8)];
+  constexpr int LD = GBK + 8;  // +16 B pad per row breaks the power-of-2 stride
+  const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;  // 2x2 waves of 32x32
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < K; k0 += GBK) {
+    // 64 rows x 32 cols per operand = 2048 elems; 256 threads x 8 elems
+    {
+      const int r = tid >> 2, c = (tid & 3) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int gk = k0 + c + e;
+        const int ga = m0 + r, gb = n0 + r;
+        sA[r * LD + c + e] = (ga < M && gk < K) ? A[(int64_t)ga * lda + gk] : (uint16_t)0;
+        sB[r * LD + c + e] = (gb < N && gk < K) ? Bt[(int64_t)gb * ldb + gk] : (uint16_t)0;
+      }
+    }
+    __syncthreads();
+    bf16x8 af[2], bfr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = wm * 32 + i * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        uint16_t bits = sA[row * LD + (lane >> 4) * 8 + e];
+        af[i][e] = __builtin_bit_cast(__bf16, bits);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = wn * 32 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        uint16_t bits = sB[row * LD + (lane >> 4) * 8 + e];
+        bfr[j][e] = __builtin_bit_cast(__bf16, bits);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int col = n0 + wn * 32 + j * 16 + (lane & 15);
+        if (row < M && col < N) {
+          float v = alpha * acc[i][j][r];
+          if constexpr (OUT_BF16) {
+            uint16_t* c = (uint16_t*)C + (int64_t)row * ldc + col;
+            if (beta != 0.f) v += beta * bf16_bits_to_float(*c);
+            *c = float_to_bf16_bits(v);
+          } else {
+            float* c = (float*)C + (int64_t)row * ldc + col;
+            if (beta != 0.f) v += beta * *c;
+            *c = v;
+          }
+        }
+      }
+}
+
+// Tiled transpose of a bf16 matrix (rows x cols, row-major, ld) into
+// out[cols x rows]; used to turn a row-major B[K,N] into Bt[N,K].
+__global__ __launch_bounds__(256) void transpose_bf16(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                      int rows, int cols, int ld_in, int ld_out) {
+  __shared__ uint16_t tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+  for (int y = ty; y < 64; y += 4) {
+    const int r = r0 + y, c = c0 + tx;
+    if (r < rows && c < cols) tile[y][tx] = in[(int64_t)r * ld_in + c];
+  }
+  __syncthreads();
+  for (int y = ty; y < 64; y += 4) {
+    const int c = c0 + y, r = r0 + tx;  // out row = input column
+    if (c < cols && r < rows) out[(int64_t)c * ld_out + r] = tile[tx][y];
+  }
+}
+
+}  // namespace bk
+
+using namespace bk;
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+BK_API int bk_gemm_bf16_fast_ok(int M, int N, int K, int lda, int ldb) {
+  return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % BN == 0 && K % BK == 0 && lda % 8 == 0 && ldb % 8 == 0;
+}
+
+// C = alpha * A . Bt^T + beta * C.  out_dtype: kBF16 or kF32.
+BK_API int bk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                           float alpha, float beta, int out_dtype, hipStream_t stream) {
+  if (!A || !Bt || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N) return kBadArgument;
+  if (out_dtype != kBF16 && out_dtype != kF32) return kBadArgument;
+  const bool fast = bk_gemm_bf16_fast_ok(M, N, K, lda, ldb) && aligned16(A) && aligned16(Bt);
+  if (fast) {
+    const unsigned grid = (unsigned)((M / BM) * (N / BN));
+    if (out_dtype == kBF16)
+      gemm_bf16_tn_fast<true><<<grid, kGemmThreads, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N, K,
+                                                                 lda, ldb, ldc, alpha, beta);
+    else
+      gemm_bf16_tn_fast<false><<<grid, kGemmThreads, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N,
+                                                                  K, lda, ldb, ldc, alpha, beta);
+  } else {
+    dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
+    if (out_dtype == kBF16)
+      gemm_bf16_tn_generic<true><<<grid, 256, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N, K, lda,
+                                                           ldb, ldc, alpha, beta);
+    else
+      gemm_bf16_tn_generic<false><<<grid, 256, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N, K, lda,
+                                                            ldb, ldc, alpha, beta);
+  }
+  return launch_status();
+}
+
+BK_API int bk_transpose_bf16(const void* in, void* out, int rows, int cols, int ld_in, int ld_out,
+                             hipStream_t stream) {
+  if (!in || !out || rows <= 0 || cols <= 0 || ld_in < cols || ld_out < rows) return kBadArgument;
+  dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+  transpose_bf16<<<grid, 256, 0, stream>>>((const uint16_t*)in, (uint16_t*)out, rows, cols, ld_in, ld_out);
+  return launch_status();
+}

@@ -1,0 +1,153 @@
+// Counter-based Philox4x32-10 uniform generator: replaces numpy.random.rand
+// in the benchmark payload (`examples/benchmark-numpy.py:20`, 1e8 f64).
+//
+// Element i of the stream depends only on (seed, i), never on the grid, so
+// results are reproducible across launch shapes and GPU counts.  One Philox
+// call yields 128 random bits = 2 f64 (numpy's 53-bit construction from two
+// 32-bit draws, a>>5 and b>>6) or 4 f32 (24-bit), written with one 16-byte
+// store per lane; the kernel is HBM-write bound (800 MB for 1e8 f64).
+#include "bk_common.hpp"
+
+namespace bk {
+
+struct Philox {
+  static constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  static constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+
+  __device__ __forceinline__ static uint4 run(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+      const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+      c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+      k0 += W0;
+      k1 += W1;
+    }
+    return c;
+  }
+};
+
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+__device__ __forceinline__ float u24(uint32_t a) { return (float)(a >> 8) * (1.0f / 16777216.0f); }
+
+// out[i] = U[0,1) (f64), scaled to [lo, hi).  Each counter value -> 2 doubles.
+__global__ __launch_bounds__(256) void philox_uniform_f64(double* __restrict__ out, int64_t n, uint32_t k0,
+                                                          uint32_t k1, uint64_t offset, double lo, double span) {
+  const int64_t pairs = (n + 1) / 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < pairs; p += stride) {
+    const uint64_t ctr = offset + (uint64_t)p;
+    const uint4 r = Philox::run(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), 0x62656b65u, 0u), k0, k1);
+    double2 v = make_double2(lo + span * u53(r.x, r.y), lo + span * u53(r.z, r.w));
+    const int64_t i = 2 * p;
+    if (i + 1 < n) {
+      *reinterpret_cast<double2*>(out + i) = v;  // 16-B store
+    } else {
+      out[i] = v.x;
+    }
+  }
+}
+
+// f32: each counter value -> 4 floats, one 16-B store.
+__global__ __launch_bounds__(256) void philox_uniform_f32(float* __restrict__ out, int64_t n, uint32_t k0, uint32_t k1,
+                                                          uint64_t offset, float lo, float span) {
+  const int64_t quads = (n + 3) / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += stride) {
+    const uint64_t ctr = offset + (uint64_t)q;
+    const uint4 r = Philox::run(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), 0x62656b66u, 0u), k0, k1);
+    float4 v = make_float4(lo + span * u24(r.x), lo + span * u24(r.y), lo + span * u24(r.z), lo + span * u24(r.w));
+    const int64_t i = 4 * q;
+    if (i + 3 < n) {
+      *reinterpret_cast<float4*>(out + i) = v;
+    } else {
+      const float t[4] = {v.x, v.y, v.z, v.w};
+      for (int j = 0; i + j < n; ++j) out[i + j] = t[j];
+    }
+  }
+}
+
+// Standard normal via Box-Muller on the f32 / f64 streams (for randn).
+__global__ __launch_bounds__(256) void philox_normal_f32(float* __restrict__ out, int64_t n, uint32_t k0, uint32_t k1,
+                                                         uint64_t offset, float mean, float std) {
+  const int64_t quads = (n + 3) / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += stride) {
+    const uint64_t ctr = offset + (uint64_t)q;
+    const uint4 r = Philox::run(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), 0x6e6f726du, 0u), k0, k1);
+    const float u1 = fmaxf(u24(r.x), 1e-12f), u2 = u24(r.y), u3 = fmaxf(u24(r.z), 1e-12f), u4 = u24(r.w);
+    const float r1 = sqrtf(-2.f * __logf(u1)), r2 = sqrtf(-2.f * __logf(u3));
+    float s1, c1, s2, c2;
+    __sincosf(6.283185307f * u2, &s1, &c1);
+    __sincosf(6.283185307f * u4, &s2, &c2);
+    const float t[4] = {mean + std * r1 * c1, mean + std * r1 * s1, mean + std * r2 * c2, mean + std * r2 * s2};
+    const int64_t i = 4 * q;
+    if (i + 3 < n) {
+      *reinterpret_cast<float4*>(out + i) = make_float4(t[0], t[1], t[2], t[3]);
+    } else {
+      for (int j = 0; i + j < n; ++j) out[i + j] = t[j];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void philox_normal_f64(double* __restrict__ out, int64_t n, uint32_t k0, uint32_t k1,
+                                                         uint64_t offset, double mean, double std) {
+  const int64_t pairs = (n + 1) / 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < pairs; p += stride) {
+    const uint64_t ctr = offset + (uint64_t)p;
+    const uint4 r = Philox::run(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), 0x6e6f726eu, 0u), k0, k1);
+    const double u1 = fmax(u53(r.x, r.y), 1e-300), u2 = u53(r.z, r.w);
+    const double rad = sqrt(-2.0 * log(u1));
+    double s, c;
+    sincos(6.283185307179586 * u2, &s, &c);
+    const int64_t i = 2 * p;
+    if (i + 1 < n) {
+      *reinterpret_cast<double2*>(out + i) = make_double2(mean + std * rad * c, mean + std * rad * s);
+    } else {
+      out[i] = mean + std * rad * c;
+    }
+  }
+}
+
+}  // namespace bk
+
+using namespace bk;
+
+// dtype: kF64 or kF32.  `offset` advances the counter so successive draws from
+// one seed never overlap (the Python side keeps the running offset).
+BK_API int bk_rand_uniform(void* out, int64_t n, int dtype, uint64_t seed, uint64_t offset, double lo, double hi,
+                           hipStream_t stream) {
+  if (!out || n < 0) return kBadArgument;
+  if (n == 0) return kOk;
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  if (dtype == kF64) {
+    const int64_t pairs = (n + 1) / 2;
+    philox_uniform_f64<<<stream_grid(pairs, 256), 256, 0, stream>>>((double*)out, n, k0, k1, offset, lo, hi - lo);
+  } else if (dtype == kF32) {
+    const int64_t quads = (n + 3) / 4;
+    philox_uniform_f32<<<stream_grid(quads, 256), 256, 0, stream>>>((float*)out, n, k0, k1, offset, (float)lo,
+                                                                    (float)(hi - lo));
+  } else {
+    return kBadArgument;
+  }
+  return launch_status();
+}
+
+BK_API int bk_rand_normal(void* out, int64_t n, int dtype, uint64_t seed, uint64_t offset, double mean, double std,
+                          hipStream_t stream) {
+  if (!out || n < 0) return kBadArgument;
+  if (n == 0) return kOk;
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  if (dtype == kF64) {
+    philox_normal_f64<<<stream_grid((n + 1) / 2, 256), 256, 0, stream>>>((double*)out, n, k0, k1, offset, mean, std);
+  } else if (dtype == kF32) {
+    philox_normal_f32<<<stream_grid((n + 3) / 4, 256), 256, 0, stream>>>((float*)out, n, k0, k1, offset, (float)mean,
+                                                                         (float)std);
+  } else {
+    return kBadArgument;
+  }
+  return launch_status();
+}

@@ -1,0 +1,183 @@
+"""Numerics of the hand-written HIP kernels vs plain fp32/fp64 references.
+
+Run on an MI355X: ``python -m pytest tests -m gpu``.  Each kernel is checked
+against numpy / torch computed in fp32 (bf16 inputs) or fp64.
+"""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_library_is_native(gpu):
+    from bee_code_interpreter_fs_amd.ops import _native
+
+    assert _native.is_loaded()
+    info = gpu.device_info()
+    assert info["arch"].startswith("gfx950"), info
+    assert info["compute_units"] >= 256
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+@pytest.mark.parametrize("n", [1, 7, 1000, 1 << 20, 10_000_019])
+def test_uniform_range_and_moments(gpu, dtype, n):
+    x = gpu.random.default_rng(1234).random(n, dtype=dtype)
+    h = x.numpy()
+    assert h.shape == (n,) and h.dtype == np.dtype(dtype)
+    assert (h >= 0).all() and (h < 1).all()
+    if n >= 1 << 20:
+        assert abs(h.mean() - 0.5) < 2e-3
+        assert abs(h.var() - 1 / 12) < 2e-3
+    # counter-based: same seed -> same stream, independent of call grouping
+    y = gpu.random.default_rng(1234).random(n, dtype=dtype).numpy()
+    np.testing.assert_array_equal(h, y)
+
+
+def test_uniform_offsets_do_not_overlap(gpu):
+    g = gpu.random.default_rng(7)
+    a = g.random(1000).numpy()
+    b = g.random(1000).numpy()
+    assert not np.array_equal(a, b)
+    c = gpu.random.default_rng(7).random(2000).numpy()
+    np.testing.assert_array_equal(np.concatenate([a, b]), c)
+
+
+def test_normal_moments(gpu):
+    x = gpu.random.default_rng(3).normal(2.0, 3.0, 1 << 22, dtype="float32").numpy()
+    assert abs(x.mean() - 2.0) < 0.02 and abs(x.std() - 3.0) < 0.02
+    y = gpu.random.default_rng(3).normal(0.0, 1.0, 1 << 21, dtype="float64").numpy()
+    assert abs(y.mean()) < 0.01 and abs(y.std() - 1.0) < 0.01
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32", "bfloat16"])
+@pytest.mark.parametrize("n", [1, 33, 4097, 3_000_001])
+def test_unary_ops(gpu, dtype, n):
+    rng = np.random.default_rng(0)
+    h = rng.uniform(0.1, 2.0, n).astype(np.float64 if dtype == "float64" else np.float32)
+    x = gpu.asarray(h, dtype=dtype)
+    ref_in = x.numpy().astype(np.float64)
+    tol = {"float64": 1e-12, "float32": 2e-6, "bfloat16": 1e-2}[dtype]
+    for name, ref in [("sqrt", np.sqrt), ("exp", np.exp), ("log", np.log), ("abs", np.abs), ("tanh", np.tanh)]:
+        out = getattr(gpu, name)(x).numpy().astype(np.float64)
+        np.testing.assert_allclose(out, ref(ref_in), rtol=tol * 4, atol=tol, err_msg=name)
+    sq = gpu.square(x).numpy().astype(np.float64)  # lazy -> materialised
+    np.testing.assert_allclose(sq, ref_in * ref_in, rtol=tol * 4, atol=tol)
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32", "bfloat16"])
+def test_binary_ops(gpu, dtype):
+    rng = np.random.default_rng(1)
+    a_h, b_h = rng.uniform(0.5, 2, 100_003), rng.uniform(0.5, 2, 100_003)
+    a, b = gpu.asarray(a_h, dtype=dtype), gpu.asarray(b_h, dtype=dtype)
+    ra, rb = a.numpy().astype(np.float64), b.numpy().astype(np.float64)
+    tol = {"float64": 1e-12, "float32": 2e-6, "bfloat16": 1e-2}[dtype]
+    for got, ref in [
+        (a + b, ra + rb),
+        (a - b, ra - rb),
+        (a * b, ra * rb),
+        (a / b, ra / rb),
+        (a * 3.0, ra * 3.0),
+        (2.0 - a, 2.0 - ra),
+        (1.0 / a, 1.0 / ra),
+        (gpu.maximum(a, b), np.maximum(ra, rb)),
+    ]:
+        np.testing.assert_allclose(got.numpy().astype(np.float64), ref, rtol=tol * 4, atol=tol)
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32", "bfloat16"])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1 << 16, 12_345_679])
+def test_reductions(gpu, dtype, n):
+    rng = np.random.default_rng(n)
+    h = rng.standard_normal(n)
+    x = gpu.asarray(h, dtype=dtype)
+    r = x.numpy().astype(np.float64)
+    rtol = 1e-10 if dtype == "float64" else 1e-6
+    scale = np.abs(r).sum() + 1e-30
+    assert abs(gpu.sum(x) - r.sum()) <= rtol * scale
+    assert abs(gpu.square_sum(x) - (r * r).sum()) <= rtol * (r * r).sum()
+    assert abs(gpu.sum(gpu.square(x)) - (r * r).sum()) <= rtol * (r * r).sum()  # fused path
+    assert gpu.amax(x) == r.max() and gpu.amin(x) == r.min()
+    y = gpu.asarray(rng.standard_normal(n), dtype=dtype)
+    ry = y.numpy().astype(np.float64)
+    assert abs(gpu.dot(x, y) - (r * ry).sum()) <= rtol * (np.abs(r * ry).sum() + 1e-30)
+
+
+def test_reduction_is_deterministic(gpu):
+    x = gpu.random.default_rng(5).random(10_000_000)
+    vals = {float(gpu.sum(x)) for _ in range(5)}
+    assert len(vals) == 1
+
+
+def test_benchmark_numpy_payload(gpu):
+    """benchmark-numpy.py semantics: E[sum(U^2)] = n/3."""
+    n = 10**8
+    x = gpu.random.rand(n)
+    s = gpu.sum(gpu.square(x))
+    assert abs(s - n / 3) < 5 * np.sqrt(n * 4 / 45)
+
+
+def _bf16_round(a):
+    import torch
+
+    return torch.from_numpy(a).to(torch.bfloat16).to(torch.float32).numpy()
+
+
+@pytest.mark.parametrize(
+    "m,n,k",
+    [(128, 128, 64), (256, 384, 512), (1024, 1024, 1024), (100, 70, 33), (129, 257, 65), (4096, 4096, 4096)],
+)
+@pytest.mark.parametrize("out_dtype", ["float32", "bfloat16"])
+def test_gemm_bf16(gpu, m, n, k, out_dtype):
+    rng = np.random.default_rng(m * 7 + n * 3 + k)
+    a_h = _bf16_round(rng.uniform(-1, 1, (m, k)).astype(np.float32))
+    b_h = _bf16_round(rng.uniform(-1, 1, (k, n)).astype(np.float32))
+    a, b = gpu.asarray(a_h, "bfloat16"), gpu.asarray(b_h, "bfloat16")
+    c = gpu.matmul(a, b, out_dtype=out_dtype).numpy().astype(np.float64)
+    ref = a_h.astype(np.float64) @ b_h.astype(np.float64)
+    atol = 2e-3 * np.sqrt(k) if out_dtype == "float32" else 1e-2 * np.abs(ref).max()
+    np.testing.assert_allclose(c, ref, rtol=1e-2, atol=atol)
+
+
+def test_gemm_asymmetric_identity(gpu):
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    n = 256
+    b_h = _bf16_round(np.arange(n * n, dtype=np.float32).reshape(n, n) % 97 / 97.0)
+    eye = gpu.asarray(np.eye(n, dtype=np.float32), "bfloat16")
+    c = gpu.matmul(eye, gpu.asarray(b_h, "bfloat16"), out_dtype="float32").numpy()
+    np.testing.assert_array_equal(c, b_h)
+    ct = gpu.matmul(gpu.asarray(b_h, "bfloat16"), eye, out_dtype="float32").numpy()
+    np.testing.assert_array_equal(ct, b_h)
+
+
+def test_gemm_transposed_view_operand(gpu):
+    rng = np.random.default_rng(11)
+    a_h = _bf16_round(rng.uniform(-1, 1, (256, 512)).astype(np.float32))
+    bt_h = _bf16_round(rng.uniform(-1, 1, (384, 512)).astype(np.float32))
+    a, bt = gpu.asarray(a_h, "bfloat16"), gpu.asarray(bt_h, "bfloat16")
+    c = gpu.matmul(a, bt.T, out_dtype="float32").numpy()
+    np.testing.assert_allclose(c, a_h.astype(np.float64) @ bt_h.T.astype(np.float64), rtol=1e-2, atol=5e-2)
+
+
+def test_quota_enforced(gpu):
+    from bee_code_interpreter_fs_amd.ops import QuotaExceeded
+
+    before = gpu.memory_stats()
+    gpu.set_quota(before["in_use"] + (64 << 20))
+    try:
+        keep = gpu.empty((1 << 20,), "float64")  # 8 MiB fits
+        with pytest.raises(QuotaExceeded):
+            gpu.empty((16 << 20,), "float64")  # 128 MiB does not
+        del keep
+    finally:
+        gpu.set_quota(0)
+
+
+def test_torch_interop(gpu):
+    import torch
+
+    t = torch.arange(1000, dtype=torch.float32, device="cuda")
+    v = gpu.from_torch(t)
+    assert float(gpu.sum(v)) == pytest.approx(float(t.sum().item()))
+    back = gpu.to_torch(gpu.square(v))
+    torch.testing.assert_close(back, t * t)
