@@ -1,0 +1,156 @@
+"""In-sandbox library patches so headless user code still produces files.
+
+Behavioural parity with the reference's ``executor/sitecustomize.py``:
+
+* ``matplotlib.pyplot.show()`` saves ``plot.png`` in the working directory
+  (`sitecustomize.py:25-28`);
+* ``PIL.ImageShow.show(img)`` saves ``image.png`` (`:38-42`);
+* ``moviepy.editor`` ``write_videofile`` is forced quiet (`:29-37`);
+* ``json`` encodes ``datetime``/``date`` as ``{"__type__": ..., "value": iso}``
+  and ``json.loads`` revives them (`:5-18`, `:43-62`).
+
+Mechanism differs: the reference swaps ``builtins.__import__`` and re-patches
+on every import statement.  Here patches are applied once — immediately for
+modules the zygote already imported, otherwise by a ``sys.meta_path`` hook
+that wraps the module's loader — so the import fast path stays untouched.
+"""
+
+from __future__ import annotations
+
+import functools
+import importlib.abc
+import importlib.util
+import json
+import sys
+from datetime import date, datetime
+from typing import Callable, Dict
+
+
+class DateTimeEncoder(json.JSONEncoder):
+    def default(self, o):
+        if isinstance(o, (datetime, date)):
+            return {"__type__": type(o).__name__, "value": o.isoformat()}
+        return super().default(o)
+
+
+def datetime_object_hook(obj: dict):
+    kind = obj.get("__type__")
+    if kind == "datetime" and "value" in obj:
+        return datetime.fromisoformat(obj["value"])
+    if kind == "date" and "value" in obj:
+        return date.fromisoformat(obj["value"])
+    return obj
+
+
+def patch_json(mod) -> None:
+    if getattr(mod, "_bee_patched", False):
+        return
+    mod.JSONEncoder = DateTimeEncoder
+    mod._default_encoder = DateTimeEncoder(
+        skipkeys=False, ensure_ascii=True, check_circular=True, allow_nan=True, indent=None, separators=None, default=None
+    )
+    original_loads = mod.loads
+
+    @functools.wraps(original_loads)
+    def loads(s, *args, **kwargs):
+        kwargs.setdefault("object_hook", datetime_object_hook)
+        return original_loads(s, *args, **kwargs)
+
+    mod.loads = loads
+    mod._bee_patched = True
+
+
+def patch_pyplot(plt) -> None:
+    if getattr(plt, "_bee_patched", False):
+        return
+
+    def show(*args, **kwargs):
+        plt.savefig("plot.png")
+
+    plt.show = show
+    plt._bee_patched = True
+
+
+def patch_pil_imageshow(imageshow) -> None:
+    if getattr(imageshow, "_bee_patched", False):
+        return
+
+    def show(image, *args, **kwargs):
+        image.save("image.png")
+        return True
+
+    imageshow.show = show
+    imageshow._bee_patched = True
+
+
+def patch_moviepy_editor(editor) -> None:
+    clip = getattr(editor, "VideoClip", None)
+    if clip is None or getattr(clip, "_bee_patched", False):
+        return
+    original = clip.write_videofile
+
+    @functools.wraps(original)
+    def write_videofile(self, *args, **kwargs):
+        kwargs["verbose"] = False
+        kwargs["logger"] = None
+        return original(self, *args, **kwargs)
+
+    clip.write_videofile = write_videofile
+    clip._bee_patched = True
+
+
+PATCHES: Dict[str, Callable] = {
+    "json": patch_json,
+    "matplotlib.pyplot": patch_pyplot,
+    "PIL.ImageShow": patch_pil_imageshow,
+    "moviepy.editor": patch_moviepy_editor,
+}
+
+
+class _PatchingLoader(importlib.abc.Loader):
+    def __init__(self, inner, patch):
+        self._inner = inner
+        self._patch = patch
+
+    def create_module(self, spec):
+        return self._inner.create_module(spec)
+
+    def exec_module(self, module):
+        self._inner.exec_module(module)
+        try:
+            self._patch(module)
+        except Exception:  # a patch must never break the user's import
+            pass
+
+
+class _PatchFinder(importlib.abc.MetaPathFinder):
+    def find_spec(self, fullname, path, target=None):
+        patch = PATCHES.get(fullname)
+        if patch is None:
+            return None
+        for finder in sys.meta_path:
+            if finder is self or not hasattr(finder, "find_spec"):
+                continue
+            spec = finder.find_spec(fullname, path, target)
+            if spec is not None and spec.loader is not None:
+                spec.loader = _PatchingLoader(spec.loader, patch)
+                return spec
+        return None
+
+
+def install() -> None:
+    for name, patch in PATCHES.items():
+        mod = sys.modules.get(name)
+        if mod is not None:
+            try:
+                patch(mod)
+            except Exception:
+                pass
+    if not any(isinstance(f, _PatchFinder) for f in sys.meta_path):
+        sys.meta_path.insert(0, _PatchFinder())
+    # PIL: the reference patches ImageShow when `PIL` itself is imported
+    if "PIL" in sys.modules and "PIL.ImageShow" not in sys.modules:
+        try:
+            import PIL.ImageShow  # noqa: F401
+        except Exception:
+            pass

@@ -1,0 +1,159 @@
+"""Sandbox zygote: pre-imports the scientific stack once, then forks workers.
+
+Started by the native executor (csrc/executor/sandbox.cpp) with a socketpair
+in ``BEE_ZYGOTE_FD``.  Line-delimited JSON protocol:
+
+  executor -> zygote   {"op": "spawn", "id", "cwd", "env"}
+  zygote -> executor   {"op": "hello", "pid", "preloaded", "import_ms"}
+                       {"op": "spawned", "id", "pid"}
+                       {"op": "spawn_failed", "id", "error"}
+                       {"op": "exit", "pid", "code", "signal"}
+
+Why: ``import torch`` alone costs ~1.5 s and the reference paid
+interpreter + imports in every fresh pod.  Forking is only safe while HIP is
+uninitialised — ``import torch`` leaves it so (verified), and nothing in this
+process ever touches the GPU; each worker initialises HIP for its own pinned
+device after the fork.  The zygote is a child subreaper, so grandchildren
+orphaned by user code are reaped here too.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import selectors
+import signal
+import socket
+import sys
+import time
+
+DEFAULT_PRELOAD = "numpy,pandas,scipy.stats,matplotlib.pyplot,PIL.Image,torch,bee_code_interpreter_fs_amd.ops"
+PR_SET_CHILD_SUBREAPER = 36
+
+
+def _preload() -> list:
+    os.environ.setdefault("MPLBACKEND", "Agg")
+    names = [n.strip() for n in os.environ.get("BEE_PRELOAD", DEFAULT_PRELOAD).split(",") if n.strip()]
+    loaded = []
+    for name in names:
+        try:
+            __import__(name)
+            loaded.append(name)
+        except Exception:
+            pass
+    # beekern: load the code object (registers kernels, does NOT init HIP)
+    if "bee_code_interpreter_fs_amd.ops" in sys.modules:
+        try:
+            from bee_code_interpreter_fs_amd.ops import _native
+
+            _native.lib()
+            loaded.append("libbeekern.so")
+        except Exception:
+            pass
+    return loaded
+
+
+def _hip_initialized() -> bool:
+    torch = sys.modules.get("torch")
+    try:
+        return bool(torch is not None and torch.cuda.is_initialized())
+    except Exception:
+        return False
+
+
+def main() -> None:
+    fd = int(os.environ["BEE_ZYGOTE_FD"])
+    chan = socket.socket(fileno=fd)
+    t0 = time.perf_counter()
+    loaded = _preload()
+    import_ms = (time.perf_counter() - t0) * 1e3
+    if _hip_initialized():
+        raise SystemExit("zygote: HIP got initialised during preload; forking would be unsafe")
+    try:
+        ctypes.CDLL(None).prctl(PR_SET_CHILD_SUBREAPER, 1, 0, 0, 0)
+    except Exception:
+        pass
+
+    def send(msg: dict) -> None:
+        chan.sendall((json.dumps(msg) + "\n").encode())
+
+    send({"op": "hello", "pid": os.getpid(), "preloaded": loaded, "import_ms": import_ms})
+
+    rfd, wfd = os.pipe()
+    os.set_blocking(wfd, False)
+    signal.set_wakeup_fd(wfd)
+    signal.signal(signal.SIGCHLD, lambda *_: None)
+    signal.signal(signal.SIGTERM, lambda *_: (_ for _ in ()).throw(SystemExit(0)))
+
+    sel = selectors.DefaultSelector()
+    sel.register(chan, selectors.EVENT_READ, "chan")
+    sel.register(rfd, selectors.EVENT_READ, "sig")
+    buf = b""
+    children = set()
+
+    def reap() -> None:
+        while True:
+            try:
+                pid, status = os.waitpid(-1, os.WNOHANG)
+            except ChildProcessError:
+                return
+            if pid == 0:
+                return
+            children.discard(pid)
+            if os.WIFSIGNALED(status):
+                send({"op": "exit", "pid": pid, "code": -1, "signal": os.WTERMSIG(status)})
+            else:
+                send({"op": "exit", "pid": pid, "code": os.WEXITSTATUS(status), "signal": 0})
+
+    try:
+        while True:
+            for key, _ in sel.select(timeout=1.0):
+                if key.data == "sig":
+                    try:
+                        os.read(rfd, 4096)
+                    except BlockingIOError:
+                        pass
+                    continue
+                data = chan.recv(65536)
+                if not data:
+                    raise SystemExit(0)
+                buf += data
+                while b"\n" in buf:
+                    line, buf = buf.split(b"\n", 1)
+                    msg = json.loads(line)
+                    if msg.get("op") != "spawn":
+                        continue
+                    try:
+                        pid = os.fork()
+                    except OSError as e:
+                        send({"op": "spawn_failed", "id": msg.get("id"), "error": str(e)})
+                        continue
+                    if pid == 0:
+                        # ---- child ----
+                        signal.set_wakeup_fd(-1)
+                        signal.signal(signal.SIGCHLD, signal.SIG_DFL)
+                        signal.signal(signal.SIGTERM, signal.SIG_DFL)
+                        sel.close()
+                        for f in (rfd, wfd):
+                            os.close(f)
+                        chan.close()
+                        from .worker import worker_main
+
+                        worker_main(msg)  # never returns
+                        os._exit(70)
+                    children.add(pid)
+                    send({"op": "spawned", "id": msg.get("id"), "pid": pid})
+            reap()
+    except SystemExit:
+        pass
+    finally:
+        for pid in list(children):
+            try:
+                os.killpg(pid, signal.SIGKILL)
+            except OSError:
+                pass
+
+
+if __name__ == "__main__":
+    main()

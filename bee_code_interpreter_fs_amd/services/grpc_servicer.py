@@ -1,0 +1,148 @@
+"""``code_interpreter.v1.CodeInterpreterService`` implementation.
+
+Parity with `services/grpc_servicers/code_interpreter_servicer.py:33-135`:
+per-RPC request id, request validation -> ``INVALID_ARGUMENT``, custom-tool
+errors mapped into the response ``oneof`` arms.  Differences:
+
+* ``Execute`` passes ``source_code`` through to the backend (the fork's call
+  into a ``source_file``-only executor raised ValidationError);
+* validation is hand-written (protovalidate is not on the image): file keys
+  must be normalised absolute paths, values object ids, ``executor_id`` an id;
+* unknown object ids map to ``NOT_FOUND`` instead of an opaque ``UNKNOWN``.
+"""
+
+from __future__ import annotations
+
+import json
+import logging
+import re
+import time
+
+import grpc
+
+from ..models import proto as pb
+from ..utils.logging import new_request_id
+from ..utils.validation import ValidationError, check_file_map
+from .custom_tool_executor import CustomToolExecuteError, CustomToolExecutor, CustomToolParseError
+from .metrics import METRICS
+
+logger = logging.getLogger("code_interpreter_servicer")
+
+_EXECUTOR_ID = re.compile(r"^[0-9a-zA-Z_-]{0,255}$")
+MAX_SOURCE_BYTES = 16 * 1024 * 1024
+
+
+class CodeInterpreterServicer:
+    def __init__(self, code_executor, custom_tool_executor: CustomToolExecutor) -> None:
+        self.code_executor = code_executor
+        self.custom_tool_executor = custom_tool_executor
+
+    # -- validation ------------------------------------------------------------------
+    @staticmethod
+    def _validate_execute(request) -> None:
+        errors = []
+        if not _EXECUTOR_ID.match(request.executor_id):
+            errors.append("executor_id: must match ^[0-9a-zA-Z_-]{0,255}$")
+        if len(request.source_code.encode()) > MAX_SOURCE_BYTES:
+            errors.append("source_code: too large")
+        if request.timeout < 0:
+            errors.append("timeout: must be >= 0")
+        if request.gpus < 0:
+            errors.append("gpus: must be >= 0")
+        try:
+            check_file_map(dict(request.files))
+        except ValidationError as e:
+            errors.extend(e.errors)
+        if errors:
+            raise ValidationError(errors)
+
+    async def _abort_invalid(self, context, request, e: ValidationError):
+        logger.warning("Invalid request %s: %s", type(request).__name__, e.errors)
+        await context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e.errors))
+
+    # -- RPCs -------------------------------------------------------------------------
+    async def Execute(self, request, context):
+        new_request_id()
+        t0 = time.perf_counter()
+        logger.info("Executing code with files %s", dict(request.files))
+        try:
+            self._validate_execute(request)
+        except ValidationError as e:
+            METRICS.inc("bee_rpc_total", rpc="Execute", code="INVALID_ARGUMENT")
+            await self._abort_invalid(context, request, e)
+        kwargs = {"files": dict(request.files)}
+        if request.source_file:
+            kwargs["source_file"] = request.source_file
+        else:
+            kwargs["source_code"] = request.source_code
+        if request.timeout > 0:
+            kwargs["timeout"] = request.timeout
+        if request.gpus > 0:
+            kwargs["gpus"] = request.gpus
+            if request.gpus > 1:
+                kwargs["nprocs"] = request.gpus
+        if request.hbm_bytes > 0:
+            kwargs["hbm_bytes"] = request.hbm_bytes
+        try:
+            result = await self.code_executor.execute(**kwargs)
+        except FileNotFoundError as e:
+            METRICS.inc("bee_rpc_total", rpc="Execute", code="NOT_FOUND")
+            await context.abort(grpc.StatusCode.NOT_FOUND, str(e))
+        except (ValidationError, ValueError) as e:
+            METRICS.inc("bee_rpc_total", rpc="Execute", code="INVALID_ARGUMENT")
+            await context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        except Exception as e:
+            logger.exception("Error executing code")
+            METRICS.inc("bee_rpc_total", rpc="Execute", code="INTERNAL")
+            await context.abort(grpc.StatusCode.INTERNAL, f"execution failed: {e}")
+        METRICS.inc("bee_rpc_total", rpc="Execute", code="OK")
+        METRICS.observe_ms("bee_rpc_latency_ms", (time.perf_counter() - t0) * 1e3, rpc="Execute")
+        for phase, ms in result.timings_ms.items():
+            METRICS.observe_ms("bee_execute_phase_ms", ms, phase=phase)
+        logger.info("Code execution completed with exit code %s", result.exit_code)
+        return pb.ExecuteResponse(
+            stdout=result.stdout,
+            stderr=result.stderr,
+            exit_code=result.exit_code,
+            files=result.files,
+            timings_ms=result.timings_ms,
+            gpu_ids=result.gpu_ids,
+        )
+
+    async def ParseCustomTool(self, request, context):
+        new_request_id()
+        logger.info("Parsing custom tool")
+        try:
+            tool = self.custom_tool_executor.parse(tool_source_code=request.tool_source_code)
+        except CustomToolParseError as e:
+            logger.warning("Invalid custom tool: %s", e.errors)
+            METRICS.inc("bee_rpc_total", rpc="ParseCustomTool", code="OK_ERROR_ARM")
+            return pb.ParseCustomToolResponse(error={"error_messages": e.errors})
+        METRICS.inc("bee_rpc_total", rpc="ParseCustomTool", code="OK")
+        return pb.ParseCustomToolResponse(
+            success={
+                "tool_name": tool.name,
+                "tool_input_schema_json": json.dumps(tool.input_schema),
+                "tool_description": tool.description,
+            }
+        )
+
+    async def ExecuteCustomTool(self, request, context):
+        new_request_id()
+        logger.info("Executing custom tool")
+        try:
+            tool_input = json.loads(request.tool_input_json or "{}")
+        except json.JSONDecodeError as e:
+            await context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"tool_input_json: {e}")
+        try:
+            result = await self.custom_tool_executor.execute(
+                tool_source_code=request.tool_source_code, tool_input=tool_input
+            )
+        except CustomToolExecuteError as e:
+            logger.warning("Error executing custom tool: %s", e.stderr[-500:])
+            METRICS.inc("bee_rpc_total", rpc="ExecuteCustomTool", code="OK_ERROR_ARM")
+            return pb.ExecuteCustomToolResponse(error={"stderr": e.stderr})
+        except CustomToolParseError as e:
+            await context.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e.errors))
+        METRICS.inc("bee_rpc_total", rpc="ExecuteCustomTool", code="OK")
+        return pb.ExecuteCustomToolResponse(success={"tool_output_json": json.dumps(result)})

@@ -1,0 +1,152 @@
+// Sandbox pool: single-use Python workers forked from a pre-imported zygote,
+// pinned to this executor's GPU, warmed (HIP context + kernel code object)
+// while they wait, used for exactly one execution, then destroyed.
+//
+// Replaces the reference's per-request executor pod + in-pod actix server
+// (`executor/server.rs:139-228`, `kubernetes_code_executor.py:163-279`):
+// the "pod" becomes a forked process group with a private workspace, the
+// pod pool becomes the warm-worker deque, and the per-pod upm/xonsh/python
+// cold start (~1.5 s for torch) is paid once by the zygote.
+#pragma once
+#include <sys/types.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "json.hpp"
+
+namespace bee {
+
+struct PoolConfig {
+  std::string sandbox_root = "/tmp/bee-sandboxes";
+  std::string run_dir;                 // control sockets; default <sandbox_root>/.run
+  std::string python = "python3";
+  std::string zygote_module = "bee_code_interpreter_fs_amd.runtime.zygote";
+  std::string gpus;                    // HIP_VISIBLE_DEVICES for pooled workers ("" = CPU only)
+  int target = 4;                      // warm workers kept ready
+  int max_concurrent_spawns = 8;       // HIP init contends in the driver
+  bool warm_gpu = true;
+  bool recursive_scan = false;
+  int64_t max_output_bytes = 16 << 20;
+  double default_timeout_s = 60.0;
+  double acquire_timeout_s = 120.0;
+  int64_t default_hbm_quota = 0;
+  std::string zygote_preload;          // LD_PRELOAD for the zygote (HBM interposer)
+  std::map<std::string, std::string> extra_env;
+  // pod mode: one fixed sandbox (reference k8s contract)
+  bool pod_mode = false;
+  std::string pod_workspace = "/workspace";
+  std::string pod_runtime_packages = "/runtime-packages";
+  std::string pythonpath;              // prepended to PYTHONPATH of zygote
+};
+
+enum class WorkerState { Spawning, Connected, Ready, Running, Exited, Failed };
+
+struct Worker {
+  std::string id;
+  std::string dir, ws, rp, meta;
+  std::string gpus;
+  pid_t pid = -1;
+  int fd = -1;
+  WorkerState state = WorkerState::Spawning;
+  double t_spawn = 0, t_ready = 0;
+  double warm_ms = 0;
+  bool exited = false;
+  int exit_code = 0;
+  int term_signal = 0;
+  bool pooled = true;  // false: dedicated (gang / custom env) worker
+  std::string fail_reason;
+};
+
+struct ExecTimings {
+  double acquire_ms = 0, stage_ms = 0, run_ms = 0, collect_ms = 0, total_ms = 0;
+};
+
+class SandboxPool {
+ public:
+  explicit SandboxPool(PoolConfig cfg);
+  ~SandboxPool();
+  bool start(std::string* err);
+  void stop();
+
+  // POST /v1/execute (pool mode). Returns response JSON; sets *http_status.
+  Json execute(const Json& req, int* http_status);
+  // POST /execute (pod mode, reference-compatible body {source_file, timeout}).
+  Json execute_pod(const Json& req, int* http_status);
+
+  Json status();
+  std::string metrics_text();
+  const PoolConfig& config() const { return cfg_; }
+  bool healthy() const { return zygote_alive_.load(); }
+
+ private:
+  // zygote
+  bool start_zygote(std::string* err);
+  void zygote_reader();
+  void send_zygote(const Json& msg);
+  // workers
+  void worker_acceptor();
+  void worker_reader(int fd);
+  std::shared_ptr<Worker> spawn_worker(bool pooled, const std::string& gpus, const Json& extra_env,
+                                       const std::string& fixed_ws = "", const std::string& fixed_rp = "");
+  void refill_locked();
+  std::shared_ptr<Worker> acquire(double timeout_s, std::string* err);
+  bool wait_ready(const std::shared_ptr<Worker>& w, double timeout_s);
+  void destroy(const std::shared_ptr<Worker>& w);
+  void cleanup_loop();
+
+  struct RunSpec {
+    std::string script;
+    std::vector<std::string> argv;
+    double timeout_s = 60;
+    int64_t hbm_quota = 0;
+    Json env = Json::object();
+  };
+  struct RunResult {
+    std::string stdout_text, stderr_text;
+    int exit_code = 0;
+    bool timed_out = false;
+    bool died = false;  // worker vanished before running (spawn/warm failure)
+  };
+  RunResult run_in(const std::shared_ptr<Worker>& w, const RunSpec& spec);
+  Json run_job(const Json& req, int* http_status, bool pod);
+
+  PoolConfig cfg_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::map<std::string, std::shared_ptr<Worker>> workers_;  // by id
+  std::map<pid_t, std::shared_ptr<Worker>> by_pid_;
+  std::deque<std::shared_ptr<Worker>> ready_;
+  int spawning_ = 0;
+  int inflight_spawns_ = 0;
+  std::deque<std::pair<std::shared_ptr<Worker>, Json>> spawn_queue_;
+
+  pid_t zygote_pid_ = -1;
+  int zygote_fd_ = -1;
+  std::mutex zygote_write_mu_;
+  std::atomic<bool> zygote_alive_{false};
+  std::atomic<bool> stopping_{false};
+  int worker_listen_fd_ = -1;
+  std::string worker_sock_path_;
+  std::thread zygote_thread_, acceptor_thread_, cleanup_thread_;
+  std::mutex cleanup_mu_;
+  std::condition_variable cleanup_cv_;
+  std::deque<std::string> cleanup_dirs_;
+  std::mutex pod_mu_;  // pod mode: one execution at a time
+
+  // metrics
+  std::atomic<int64_t> m_exec_total_{0}, m_exec_failed_{0}, m_timeouts_{0}, m_spawned_{0}, m_spawn_failed_{0};
+  std::atomic<int64_t> m_inflight_{0};
+  double m_warm_ms_sum_ = 0, m_exec_ms_sum_ = 0, m_acquire_ms_sum_ = 0;
+  int64_t m_warm_count_ = 0;
+};
+
+}  // namespace bee

@@ -1,0 +1,305 @@
+#include "util.hpp"
+
+#include <dirent.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <ftw.h>
+#include <stdarg.h>
+#include <sys/random.h>
+#include <sys/sendfile.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+
+namespace bee {
+
+static std::mutex g_log_mu;
+
+void log_line(const char* level, const char* fmt, ...) {
+  char msg[4096];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(msg, sizeof msg, fmt, ap);
+  va_end(ap);
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  struct tm tm;
+  gmtime_r(&ts.tv_sec, &tm);
+  std::lock_guard<std::mutex> lk(g_log_mu);
+  fprintf(stderr, "[%04d-%02d-%02dT%02d:%02d:%02d.%03ldZ %s bee-executor] %s\n", tm.tm_year + 1900, tm.tm_mon + 1,
+          tm.tm_mday, tm.tm_hour, tm.tm_min, tm.tm_sec, ts.tv_nsec / 1000000, level, msg);
+  fflush(stderr);
+}
+
+int64_t wall_ns() {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return (int64_t)ts.tv_sec * 1000000000LL + ts.tv_nsec;
+}
+
+double mono_ms() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+}
+
+std::string random_hex(size_t nbytes) {
+  std::vector<unsigned char> buf(nbytes);
+  size_t got = 0;
+  while (got < nbytes) {
+    ssize_t r = getrandom(buf.data() + got, nbytes - got, 0);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      // extremely unlikely; fall back to a time-seeded mix rather than abort
+      for (size_t i = got; i < nbytes; ++i) buf[i] = (unsigned char)((wall_ns() >> (i % 8)) ^ (i * 131));
+      break;
+    }
+    got += (size_t)r;
+  }
+  static const char* hex = "0123456789abcdef";
+  std::string out;
+  out.reserve(nbytes * 2);
+  for (unsigned char c : buf) {
+    out += hex[c >> 4];
+    out += hex[c & 15];
+  }
+  return out;
+}
+
+bool mkdirs(const std::string& path, mode_t mode) {
+  if (path.empty()) return false;
+  std::string cur;
+  size_t i = 0;
+  while (i <= path.size()) {
+    size_t j = path.find('/', i);
+    if (j == std::string::npos) j = path.size();
+    cur = path.substr(0, j);
+    if (!cur.empty()) {
+      if (mkdir(cur.c_str(), mode) != 0 && errno != EEXIST) return false;
+    }
+    i = j + 1;
+  }
+  struct stat st;
+  return stat(path.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+
+static int rm_cb(const char* p, const struct stat*, int, struct FTW*) {
+  remove(p);
+  return 0;
+}
+
+void rm_rf(const std::string& path) {
+  if (path.empty() || path == "/") return;
+  nftw(path.c_str(), rm_cb, 64, FTW_DEPTH | FTW_PHYS);
+}
+
+bool copy_file(const std::string& src, const std::string& dst, std::string* err) {
+  int in = open(src.c_str(), O_RDONLY | O_CLOEXEC);
+  if (in < 0) {
+    if (err) *err = "open " + src + ": " + strerror(errno);
+    return false;
+  }
+  struct stat st;
+  fstat(in, &st);
+  int out = open(dst.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (out < 0) {
+    if (err) *err = "open " + dst + ": " + strerror(errno);
+    close(in);
+    return false;
+  }
+  int64_t left = st.st_size;
+  bool ok = true;
+  while (left > 0) {
+    ssize_t n = copy_file_range(in, nullptr, out, nullptr, (size_t)left, 0);
+    if (n > 0) {
+      left -= n;
+      continue;
+    }
+    if (n < 0 && errno == EINTR) continue;
+    // EXDEV/ENOSYS/0: fall back to sendfile, then read/write
+    off_t off = st.st_size - left;
+    ssize_t m = sendfile(out, in, &off, (size_t)left);
+    if (m > 0) {
+      left -= m;
+      continue;
+    }
+    char buf[1 << 16];
+    lseek(in, st.st_size - left, SEEK_SET);
+    ssize_t r = read(in, buf, sizeof buf);
+    if (r <= 0 || !write_all(out, buf, (size_t)r)) {
+      ok = false;
+      if (err) *err = "copy " + src + " -> " + dst + ": " + strerror(errno);
+      break;
+    }
+    left -= r;
+  }
+  close(in);
+  if (close(out) != 0) ok = false;
+  return ok;
+}
+
+bool link_or_copy(const std::string& src, const std::string& dst, std::string* err) {
+  if (link(src.c_str(), dst.c_str()) == 0) return true;
+  return copy_file(src, dst, err);
+}
+
+bool write_file(const std::string& path, const std::string& data, std::string* err) {
+  int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) {
+    if (err) *err = "open " + path + ": " + strerror(errno);
+    return false;
+  }
+  bool ok = write_all(fd, data);
+  if (close(fd) != 0) ok = false;
+  if (!ok && err) *err = "write " + path + ": " + strerror(errno);
+  return ok;
+}
+
+std::string read_file_capped(const std::string& path, int64_t max_bytes, bool* truncated) {
+  if (truncated) *truncated = false;
+  int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return "";
+  std::string out;
+  char buf[1 << 16];
+  while (true) {
+    ssize_t r = read(fd, buf, sizeof buf);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) break;
+    int64_t room = max_bytes - (int64_t)out.size();
+    if (room <= 0) {
+      if (truncated) *truncated = true;
+      break;
+    }
+    out.append(buf, (size_t)(r < room ? r : room));
+    if (r > room) {
+      if (truncated) *truncated = true;
+      break;
+    }
+  }
+  close(fd);
+  return out;
+}
+
+bool is_regular_file(const std::string& path) {
+  struct stat st;
+  return stat(path.c_str(), &st) == 0 && S_ISREG(st.st_mode);
+}
+
+std::string dirname_of(const std::string& path) {
+  size_t p = path.rfind('/');
+  if (p == std::string::npos) return ".";
+  if (p == 0) return "/";
+  return path.substr(0, p);
+}
+
+std::string join_path(const std::string& a, const std::string& b) {
+  if (a.empty()) return b;
+  if (b.empty()) return a;
+  if (a.back() == '/') return a + b;
+  return a + "/" + b;
+}
+
+static void scan_dir(const std::string& root, const std::string& rel, bool recursive,
+                     std::map<std::string, FileStamp>& out, int depth) {
+  if (depth > 64) return;
+  std::string dir = rel.empty() ? root : join_path(root, rel);
+  DIR* d = opendir(dir.c_str());
+  if (!d) return;
+  while (struct dirent* e = readdir(d)) {
+    if (!strcmp(e->d_name, ".") || !strcmp(e->d_name, "..")) continue;
+    std::string r = rel.empty() ? std::string(e->d_name) : rel + "/" + e->d_name;
+    struct stat st;
+    if (lstat(join_path(root, r).c_str(), &st) != 0) continue;
+    if (S_ISREG(st.st_mode)) {
+      FileStamp fs;
+      fs.ino = st.st_ino;
+      fs.size = st.st_size;
+      fs.mtime_ns = (int64_t)st.st_mtim.tv_sec * 1000000000LL + st.st_mtim.tv_nsec;
+      fs.ctime_ns = (int64_t)st.st_ctim.tv_sec * 1000000000LL + st.st_ctim.tv_nsec;
+      out[r] = fs;
+    } else if (S_ISDIR(st.st_mode) && recursive) {
+      scan_dir(root, r, recursive, out, depth + 1);
+    }
+  }
+  closedir(d);
+}
+
+std::map<std::string, FileStamp> scan_files(const std::string& root, bool recursive) {
+  std::map<std::string, FileStamp> out;
+  scan_dir(root, "", recursive, out, 0);
+  return out;
+}
+
+bool split_logical(const std::string& logical, std::string* root, std::string* rel, std::string* err) {
+  auto bad = [&](const char* why) {
+    if (err) *err = "invalid path " + logical + ": " + why;
+    return false;
+  };
+  if (logical.size() < 2 || logical[0] != '/' || logical[1] == '/') return bad("must be absolute (^/[^/].*$)");
+  if (logical.find('\0') != std::string::npos) return bad("NUL byte");
+  // reject '.', '..' and empty segments
+  size_t i = 1;
+  while (i <= logical.size()) {
+    size_t j = logical.find('/', i);
+    if (j == std::string::npos) j = logical.size();
+    std::string seg = logical.substr(i, j - i);
+    if (seg.empty() && j != logical.size()) return bad("empty segment");
+    if (seg == "." || seg == "..") return bad("'.' or '..' segment");
+    i = j + 1;
+  }
+  std::string p = logical;
+  while (p.size() > 1 && p.back() == '/') p.pop_back();
+  static const std::string kWs = "/workspace", kRp = "/runtime-packages";
+  if (p == kWs || p == kRp) return bad("names a root directory");
+  if (p.compare(0, kRp.size() + 1, kRp + "/") == 0) {
+    *root = "runtime-packages";
+    *rel = p.substr(kRp.size() + 1);
+  } else if (p.compare(0, kWs.size() + 1, kWs + "/") == 0) {
+    *root = "workspace";
+    *rel = p.substr(kWs.size() + 1);
+  } else {
+    *root = "workspace";
+    *rel = p.substr(1);
+  }
+  return !rel->empty() || bad("empty");
+}
+
+std::string url_decode(const std::string& s) {
+  std::string out;
+  out.reserve(s.size());
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size() && isxdigit((unsigned char)s[i + 1]) && isxdigit((unsigned char)s[i + 2])) {
+      out += (char)strtol(s.substr(i + 1, 2).c_str(), nullptr, 16);
+      i += 2;
+    } else {
+      out += s[i];
+    }
+  }
+  return out;
+}
+
+void set_cloexec(int fd) {
+  int flags = fcntl(fd, F_GETFD);
+  if (flags >= 0) fcntl(fd, F_SETFD, flags | FD_CLOEXEC);
+}
+
+bool write_all(int fd, const char* data, size_t n) {
+  while (n > 0) {
+    ssize_t w = write(fd, data, n);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    data += w;
+    n -= (size_t)w;
+  }
+  return true;
+}
+
+bool write_all(int fd, const std::string& s) { return write_all(fd, s.data(), s.size()); }
+
+}  // namespace bee

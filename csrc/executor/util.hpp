@@ -1,0 +1,63 @@
+// Filesystem / process / logging helpers for the executor daemon.
+#pragma once
+#include <sys/types.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace bee {
+
+// ---- logging ------------------------------------------------------------
+void log_line(const char* level, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+#define BEE_INFO(...) ::bee::log_line("INFO", __VA_ARGS__)
+#define BEE_WARN(...) ::bee::log_line("WARN", __VA_ARGS__)
+#define BEE_ERROR(...) ::bee::log_line("ERROR", __VA_ARGS__)
+
+// ---- time -----------------------------------------------------------------
+int64_t wall_ns();     // CLOCK_REALTIME
+double mono_ms();      // CLOCK_MONOTONIC, milliseconds
+
+// ---- ids ------------------------------------------------------------------
+std::string random_hex(size_t nbytes);  // getrandom(2)-backed
+
+// ---- fs -------------------------------------------------------------------
+bool mkdirs(const std::string& path, mode_t mode = 0755);
+void rm_rf(const std::string& path);
+bool copy_file(const std::string& src, const std::string& dst, std::string* err);
+// hard link (same fs) else copy
+bool link_or_copy(const std::string& src, const std::string& dst, std::string* err);
+bool write_file(const std::string& path, const std::string& data, std::string* err);
+std::string read_file_capped(const std::string& path, int64_t max_bytes, bool* truncated);
+bool is_regular_file(const std::string& path);
+std::string dirname_of(const std::string& path);
+std::string join_path(const std::string& a, const std::string& b);
+
+struct FileStamp {
+  uint64_t ino = 0;
+  int64_t size = 0;
+  int64_t mtime_ns = 0;
+  int64_t ctime_ns = 0;
+  bool operator==(const FileStamp& o) const {
+    return ino == o.ino && size == o.size && mtime_ns == o.mtime_ns && ctime_ns == o.ctime_ns;
+  }
+};
+// regular files below `root` (top level only unless recursive), keyed by path
+// relative to root.  Symlinks are not followed.
+std::map<std::string, FileStamp> scan_files(const std::string& root, bool recursive);
+
+// ---- logical sandbox paths ------------------------------------------------
+// "/workspace/a/b" -> ("workspace", "a/b"); "/runtime-packages/x" ->
+// ("runtime-packages", "x"); any other absolute path lands in the workspace.
+// Rejects relative paths, '..', '.', '//' and root directories.
+bool split_logical(const std::string& logical, std::string* root, std::string* rel, std::string* err);
+
+std::string url_decode(const std::string& s);
+
+// ---- process --------------------------------------------------------------
+void set_cloexec(int fd);
+bool write_all(int fd, const char* data, size_t n);
+bool write_all(int fd, const std::string& s);
+
+}  // namespace bee

@@ -1,0 +1,385 @@
+"""End-to-end service tests on CPU: the full stack (gRPC + REST -> local pool
+-> native bee-executor -> zygote-forked sandbox) with sync clients.
+
+Mirrors the reference's black-box suites (`test/e2e/test_grpc.py`,
+`test/e2e/test_http.py`) case by case, for both APIs.
+``test_ad_hoc_import`` needs ``pip install cowsay`` from a package index,
+which does not exist on these machines; it runs against a local wheelhouse
+when ``BEE_TEST_WHEELHOUSE`` points at one and is skipped otherwise.
+"""
+
+import json
+import os
+import textwrap
+
+import grpc
+import httpx
+import pytest
+
+from bee_code_interpreter_fs_amd.models import proto as pb
+
+from .harness import ServiceHarness, ensure_native_executor
+
+USING_IMPORTS = textwrap.dedent(
+    """
+    import numpy as np
+    import pandas as pd
+    from scipy.stats import ttest_ind
+
+    rng = np.random.default_rng(7)
+    a = rng.normal(10, 2, 200)
+    b = rng.normal(12, 2, 200)
+    print("Means:", pd.Series(a).mean(), pd.Series(b).mean())
+    t, p = ttest_ind(a, b)
+    print("T-Statistic:", t)
+    print("P-Value:", p)
+    """
+)
+
+MY_TOOL = '''
+def my_tool(a: int, b: typing.Tuple[Optional[str], str] = ("hello", "world"), *, c: typing.Union[list[str], dict[str, typing.Optional[float]]]) -> int:
+    """
+    This tool is really really cool.
+    Very toolish experience:
+    - Toolable.
+    - Toolastic.
+    - Toolicious.
+    :param a: something cool
+    (very cool indeed)
+    :param b: something nice
+    :return: something great
+    :param c: something awful
+    """
+    return 1 + 1
+'''
+
+MY_TOOL_SCHEMA = {
+    "$schema": "http://json-schema.org/draft-07/schema#",
+    "type": "object",
+    "title": "my_tool",
+    "properties": {
+        "a": {"type": "integer", "description": "something cool\n(very cool indeed)"},
+        "b": {
+            "type": "array",
+            "minItems": 2,
+            "items": [{"anyOf": [{"type": "null"}, {"type": "string"}]}, {"type": "string"}],
+            "additionalItems": False,
+            "description": "something nice",
+        },
+        "c": {
+            "anyOf": [
+                {"type": "array", "items": {"type": "string"}},
+                {"type": "object", "additionalProperties": {"anyOf": [{"type": "null"}, {"type": "number"}]}},
+            ],
+            "description": "something awful",
+        },
+    },
+    "required": ["a", "c"],
+    "additionalProperties": False,
+}
+MY_TOOL_DESCRIPTION = (
+    "This tool is really really cool.\nVery toolish experience:\n- Toolable.\n- Toolastic.\n- Toolicious."
+    "\n\nReturns: int -- something great"
+)
+
+WEATHER_TOOL = '''
+import typing
+import requests
+
+def current_weather(lat: float, lon: float):
+    """
+    Get the current weather at a location.
+
+    :param lat: A latitude.
+    :param lon: A longitude.
+    :return: A dictionary with the current weather.
+    """
+    url = "https://fake-api.com/weather?lat=" + str(lat) + "&lon=" + str(lon)
+    response = requests.get(url)
+    response.raise_for_status()
+    return response.json()'''
+
+BAD_TOOL = "def my_tool(a, /, b, *args, **kwargs) -> int:\n  return 1 + 1"
+BAD_TOOL_ERRORS = {
+    "The tool function must not have positional-only arguments",
+    "The tool function must not have *args",
+    "The tool function must not have **kwargs",
+    "The tool function arguments must have type annotations",
+}
+
+
+@pytest.fixture(scope="module")
+def service(tmp_path_factory):
+    ensure_native_executor()
+    h = ServiceHarness(str(tmp_path_factory.mktemp("svc")), default_timeout=30.0)
+    h.start()
+    yield h
+    h.stop()
+
+
+@pytest.fixture(scope="module")
+def stub(service):
+    channel = grpc.insecure_channel(service.grpc_target)
+    yield pb.CodeInterpreterServiceStub(channel)
+    channel.close()
+
+
+@pytest.fixture(scope="module")
+def http(service):
+    with httpx.Client(base_url=service.http_base, timeout=60) as c:
+        yield c
+
+
+# ---------------------------------------------------------------- gRPC ----
+
+def test_grpc_hello_world(stub):
+    r = stub.Execute(pb.ExecuteRequest(executor_id="health-check", source_code="print(21 * 2)"), timeout=60)
+    assert r.stdout == "42\n" and r.exit_code == 0
+
+
+def test_grpc_imports(stub):
+    r = stub.Execute(pb.ExecuteRequest(source_code=USING_IMPORTS), timeout=60)
+    assert "P-Value" in r.stdout, r.stderr
+
+
+def test_grpc_create_file_then_read_it(stub):
+    r1 = stub.Execute(pb.ExecuteRequest(source_code="with open('file.txt', 'w') as f:\n    f.write('Hello, World!')\n"))
+    assert r1.exit_code == 0
+    assert set(r1.files.keys()) == {"/workspace/file.txt"}
+    r2 = stub.Execute(
+        pb.ExecuteRequest(
+            source_code="with open('file.txt') as f:\n    print(f.read())\n",
+            files={"/workspace/file.txt": r1.files["/workspace/file.txt"]},
+        )
+    )
+    assert r2.exit_code == 0
+    assert r2.stdout == "Hello, World!\n"
+    assert not r2.files  # unchanged inputs are not reported back
+
+
+def test_grpc_crash_reports_traceback(stub):
+    r = stub.Execute(pb.ExecuteRequest(source_code="print(0/0)"))
+    assert r.exit_code == 1
+    assert "ZeroDivisionError: division by zero" in r.stderr
+    assert "Traceback" in r.stderr
+
+
+def test_grpc_timeout_is_enforced(stub):
+    r = stub.Execute(pb.ExecuteRequest(source_code="import time\nprint('x', flush=True)\ntime.sleep(30)", timeout=1.0))
+    assert r.exit_code == -1
+    assert "Execution timed out" in r.stderr
+
+
+def test_grpc_invalid_file_map(stub):
+    with pytest.raises(grpc.RpcError) as e:
+        stub.Execute(pb.ExecuteRequest(source_code="pass", files={"relative/path": "abc"}))
+    assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+    with pytest.raises(grpc.RpcError) as e:
+        stub.Execute(pb.ExecuteRequest(source_code="pass", files={"/workspace/../../etc/passwd": "abc"}))
+    assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+
+
+def test_grpc_unknown_object_is_not_found(stub):
+    with pytest.raises(grpc.RpcError) as e:
+        stub.Execute(pb.ExecuteRequest(source_code="pass", files={"/workspace/a": "deadbeef"}))
+    assert e.value.code() == grpc.StatusCode.NOT_FOUND
+
+
+def test_grpc_parse_custom_tool_success(stub):
+    r = stub.ParseCustomTool(pb.ParseCustomToolRequest(tool_source_code=MY_TOOL))
+    assert r.WhichOneof("response") == "success"
+    assert r.success.tool_name == "my_tool"
+    assert r.success.tool_description == MY_TOOL_DESCRIPTION
+    assert json.loads(r.success.tool_input_schema_json) == MY_TOOL_SCHEMA
+
+
+def test_grpc_parse_custom_tool_success_2(stub):
+    r = stub.ParseCustomTool(pb.ParseCustomToolRequest(tool_source_code=WEATHER_TOOL))
+    assert r.WhichOneof("response") == "success"
+    assert r.success.tool_name == "current_weather"
+    assert r.success.tool_description == "Get the current weather at a location.\n\nReturns: A dictionary with the current weather."
+    schema = json.loads(r.success.tool_input_schema_json)
+    assert schema["properties"] == {
+        "lat": {"type": "number", "description": "A latitude."},
+        "lon": {"type": "number", "description": "A longitude."},
+    }
+    assert schema["required"] == ["lat", "lon"]
+
+
+def test_grpc_parse_custom_tool_error(stub):
+    r = stub.ParseCustomTool(pb.ParseCustomToolRequest(tool_source_code=BAD_TOOL))
+    assert r.WhichOneof("response") == "error"
+    assert set(r.error.error_messages) == BAD_TOOL_ERRORS
+
+
+def test_grpc_execute_custom_tool_success(stub):
+    r = stub.ExecuteCustomTool(
+        pb.ExecuteCustomToolRequest(
+            tool_source_code="def adding_tool(a: int, b: int) -> int:\n  return a + b", tool_input_json='{"a": 1, "b": 2}'
+        )
+    )
+    assert r.WhichOneof("response") == "success"
+    assert r.success.tool_output_json == "3"
+
+
+def test_grpc_execute_custom_tool_error(stub):
+    r = stub.ExecuteCustomTool(
+        pb.ExecuteCustomToolRequest(
+            tool_source_code="def division_tool(a: int, b: int) -> int:\n  return a / b", tool_input_json='{"a": 0, "b": 0}'
+        )
+    )
+    assert r.WhichOneof("response") == "error"
+    assert "division by zero" in r.error.stderr
+
+
+def test_grpc_health_service(service):
+    with grpc.insecure_channel(service.grpc_target) as ch:
+        resp = pb.HealthStub(ch).Check(pb.HealthCheckRequest(service=""), timeout=10)
+        assert resp.status == 1  # SERVING
+        resp = pb.HealthStub(ch).Check(pb.HealthCheckRequest(service=pb.CI_SERVICE), timeout=10)
+        assert resp.status == 1
+        with pytest.raises(grpc.RpcError):
+            pb.HealthStub(ch).Check(pb.HealthCheckRequest(service="nope.Service"), timeout=10)
+
+
+def test_grpc_reflection_lists_and_describes(service):
+    m = pb.reflection["grpc.reflection.v1alpha"]
+    with grpc.insecure_channel(service.grpc_target) as ch:
+        call = ch.stream_stream(
+            "/grpc.reflection.v1alpha.ServerReflection/ServerReflectionInfo",
+            request_serializer=m.ServerReflectionRequest.SerializeToString,
+            response_deserializer=m.ServerReflectionResponse.FromString,
+        )
+        reqs = [
+            m.ServerReflectionRequest(list_services=""),
+            m.ServerReflectionRequest(file_containing_symbol=pb.CI_SERVICE),
+            m.ServerReflectionRequest(file_containing_symbol="code_interpreter.v1.ExecuteRequest"),
+        ]
+        out = list(call(iter(reqs), timeout=10))
+    names = {s.name for s in out[0].list_services_response.service}
+    assert pb.CI_SERVICE in names and "grpc.health.v1.Health" in names
+    from google.protobuf import descriptor_pb2
+
+    fdp = descriptor_pb2.FileDescriptorProto.FromString(out[1].file_descriptor_response.file_descriptor_proto[0])
+    assert fdp.package == "code_interpreter.v1" and fdp.service[0].name == "CodeInterpreterService"
+    assert out[2].file_descriptor_response.file_descriptor_proto
+
+
+def test_health_check_cli(service):
+    from bee_code_interpreter_fs_amd.config import Config
+    from bee_code_interpreter_fs_amd.health_check import health_check
+
+    health_check(Config(_env={}), target=service.grpc_target, timeout=60)
+
+
+# ---------------------------------------------------------------- HTTP ----
+
+def test_http_imports(http):
+    r = http.post("/v1/execute", json={"source_code": USING_IMPORTS, "files": {}})
+    assert r.status_code == 200, r.text
+    assert "P-Value" in r.json()["stdout"]
+
+
+def test_http_file_roundtrip_with_source_file(http):
+    up = http.put("/v1/files", files={"file": ("main.py", b"from pathlib import Path\nPath('out.txt').write_text('hi there')\nprint('done')\n")})
+    assert up.status_code == 200, up.text
+    script_id = up.json()["hash"]
+    r = http.post("/v1/execute", json={"source_file": "/workspace/main.py", "files": {"/workspace/main.py": script_id}})
+    assert r.status_code == 200, r.text
+    body = r.json()
+    assert body["stdout"] == "done\n" and body["exit_code"] == 0
+    assert set(body["files"]) == {"/workspace/out.txt"}  # the script itself is unchanged
+    out_id = body["files"]["/workspace/out.txt"]
+    g = http.get(f"/v1/files/{out_id}")
+    assert g.status_code == 200 and g.content == b"hi there"
+    assert g.headers["content-disposition"] == f"attachment; filename={out_id}"
+    g = http.get(f"/v1/files/{out_id}", params={"delete": "true"})
+    assert g.content == b"hi there"
+    assert http.get(f"/v1/files/{out_id}").status_code == 404
+
+
+def test_http_create_file_in_interpreter(http):
+    r1 = http.post("/v1/execute", json={"source_code": "open('file.txt','w').write('Hello, World!')", "files": {}})
+    assert r1.status_code == 200
+    files = r1.json()["files"]
+    assert set(files) == {"/workspace/file.txt"}
+    r2 = http.post("/v1/execute", json={"source_code": "print(open('file.txt').read())", "files": files})
+    assert r2.json()["stdout"] == "Hello, World!\n" and r2.json()["files"] == {}
+
+
+def test_http_delete_file(http):
+    h = http.put("/v1/files", files={"file": ("x.bin", b"\x00\x01\x02")}).json()["hash"]
+    assert http.delete(f"/v1/files/{h}").json() == {"message": "File deleted"}
+    assert http.delete(f"/v1/files/{h}").status_code == 404
+
+
+def test_http_raw_upload_large(http):
+    blob = os.urandom(3 * 1024 * 1024 + 17)
+    h = http.put("/v1/files", content=blob, headers={"content-type": "application/octet-stream"}).json()["hash"]
+    assert http.get(f"/v1/files/{h}").content == blob
+    # multipart with a body larger than one chunk and a boundary-like prefix inside
+    blob2 = b"--not-a-boundary\r\n" + os.urandom(2 * 1024 * 1024)
+    h2 = http.put("/v1/files", files={"file": ("b", blob2)}).json()["hash"]
+    assert http.get(f"/v1/files/{h2}").content == blob2
+
+
+def test_http_validation_errors(http):
+    assert http.post("/v1/execute", json={"source_file": "relative.py", "files": {}}).status_code == 422
+    assert http.post("/v1/execute", json={"files": {}}).status_code == 422
+    assert http.post("/v1/execute", json={"source_code": "pass", "files": {"/a": "bad hash!"}}).status_code == 422
+
+
+def test_http_parse_custom_tool(http):
+    r = http.post("/v1/parse-custom-tool", json={"tool_source_code": MY_TOOL})
+    assert r.status_code == 200
+    assert r.json()["tool_name"] == "my_tool"
+    assert json.loads(r.json()["tool_input_schema_json"]) == MY_TOOL_SCHEMA
+    r = http.post("/v1/parse-custom-tool", json={"tool_source_code": BAD_TOOL})
+    assert r.status_code == 400
+    assert set(r.json()["error_messages"]) == BAD_TOOL_ERRORS
+
+
+def test_http_execute_custom_tool(http):
+    r = http.post(
+        "/v1/execute-custom-tool",
+        json={"tool_source_code": "def adding_tool(a: int, b: int) -> int:\n  return a + b", "tool_input_json": '{"a": 1, "b": 2}'},
+    )
+    assert r.status_code == 200 and r.json() == {"tool_output_json": "3"}
+    r = http.post(
+        "/v1/execute-custom-tool",
+        json={"tool_source_code": "def division_tool(a: int, b: int) -> int:\n  return a / b", "tool_input_json": '{"a": 0, "b": 0}'},
+    )
+    assert r.status_code == 400 and "division by zero" in r.json()["stderr"]
+
+
+def test_http_health_metrics_status(http):
+    assert http.get("/health").json() == {"status": "SERVING"}
+    text = http.get("/metrics").text
+    assert "bee_http_requests_total" in text
+    st = http.get("/v1/status").json()
+    assert st["backend"] == "local" and st["slots"][0]["executor"]["zygote_alive"] is True
+
+
+def test_sandbox_patches_produce_files(http):
+    code = textwrap.dedent(
+        """
+        import json, datetime
+        import matplotlib.pyplot as plt
+        plt.plot([1, 2, 3], [3, 1, 2])
+        plt.show()
+        s = json.dumps({"when": datetime.date(2024, 12, 20)})
+        print(s)
+        print(type(json.loads(s)["when"]).__name__)
+        """
+    )
+    r = http.post("/v1/execute", json={"source_code": code, "files": {}}).json()
+    assert r["exit_code"] == 0, r["stderr"]
+    assert "/workspace/plot.png" in r["files"]
+    assert '{"when": {"__type__": "date", "value": "2024-12-20"}}' in r["stdout"]
+    assert r["stdout"].strip().endswith("date")
+
+
+@pytest.mark.skipif(not os.environ.get("BEE_TEST_WHEELHOUSE"), reason="needs a local wheelhouse with cowsay (no package index)")
+def test_ad_hoc_import(http):
+    r = http.post("/v1/execute", json={"source_code": "import cowsay\ncowsay.cow('Hello World')", "files": {}})
+    assert "Hello World" in r.json()["stdout"]
