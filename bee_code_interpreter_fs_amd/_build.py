@@ -71,8 +71,11 @@ def _targets() -> List[Target]:
                 output=os.path.join(PKG, "bin", "bee-executor"),
                 sources=sorted(os.path.join(ex, f) for f in os.listdir(ex) if f.endswith(".cpp")),
                 compiler=CXX,
-                compile_flags=["-O2", "-g", "-std=c++17", "-Wall", "-Wextra", "-Wno-unused-parameter", "-pthread"],
-                link_flags=["-pthread"],
+                compile_flags=[
+                    "-O2", "-g", "-std=c++17", "-Wall", "-Wextra", "-Wno-unused-parameter", "-Wno-unused-result",
+                    "-pthread", f"-I{ROCM}/include", "-D__HIP_PLATFORM_AMD__",
+                ],
+                link_flags=["-pthread", f"-L{ROCM}/lib", "-lamdhip64", "-ldl", f"-Wl,-rpath,{ROCM}/lib"],
                 shared=False,
                 headers=sorted(os.path.join(ex, f) for f in os.listdir(ex) if f.endswith(".hpp")),
             )

@@ -21,6 +21,7 @@ from .array import (  # noqa: F401
     device_info,
     divide,
     dot,
+    driver_name,
     empty,
     empty_cache,
     exp,

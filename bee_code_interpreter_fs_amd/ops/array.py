@@ -10,23 +10,23 @@ star).  The benchmark payload `examples/benchmark-numpy.py:18-22` becomes::
 
 ``square`` (and ``x * x`` / ``x ** 2``) returns a *lazy* array: if the only
 consumer is a reduction the square is fused into it (no 800 MB temporary);
-any other use materialises it with the elementwise kernel.  All kernels are
-enqueued on one stream (the HIP null stream, which torch's default stream
-also orders against), so torch tensors and DeviceArrays interleave safely.
+any other use materialises it with the elementwise kernel.
+
+Kernels run through a driver (``ops/driver.py``): in-process HIP (native) or
+the executor's kernel broker (light sandboxes, no HIP context of their own).
 """
 
 from __future__ import annotations
 
-import ctypes
 import math
 import os
 import threading
-from typing import Any, Optional, Sequence, Tuple, Union
+from typing import Any, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import _native
-from ._native import DTYPE_CODES, DTYPE_SIZES, BeekernError, check
+from ._native import DTYPE_CODES, DTYPE_SIZES, BeekernError, QuotaExceeded  # noqa: F401
+from .driver import make_driver
 
 Shape = Tuple[int, ...]
 
@@ -37,14 +37,10 @@ _UNARY = {
 _BINARY = {"add": 0, "subtract": 1, "multiply": 2, "divide": 3, "maximum": 4, "minimum": 5, "power": 6}
 _REDUCE = {"sum": 0, "square_sum": 1, "abs_sum": 2, "max": 3, "min": 4, "dot": 5}
 _SUPPORTED = ("float32", "float64", "bfloat16")
-
 _NP_DTYPES = {"float32": np.float32, "float64": np.float64}
 
 _state_lock = threading.Lock()
-_initialized_device: Optional[int] = None
-_stream = ctypes.c_void_p(0)  # HIP null stream
-_workspace: Optional["_Buffer"] = None
-_scalar_out: Optional["_Buffer"] = None
+_driver = None
 
 
 def normalize_dtype(dtype: Any) -> str:
@@ -63,80 +59,69 @@ def normalize_dtype(dtype: Any) -> str:
 
 
 def init(device: Optional[int] = None) -> int:
-    """Initialise HIP on ``device`` (default: 0 of the visible set) and load
-    the kernels; idempotent.  Sandboxes call this while waiting in the warm
-    pool so user code never pays it."""
-    global _initialized_device, _workspace, _scalar_out
-    if _initialized_device is not None:
-        return _initialized_device
+    """Initialise the driver (HIP context on ``device``, or a broker session);
+    idempotent.  Sandboxes do this while waiting in the warm pool."""
+    global _driver
+    if _driver is not None:
+        return _driver.device
     with _state_lock:
-        if _initialized_device is None:
-            dev = int(os.environ.get("BEE_DEVICE", "0")) if device is None else int(device)
-            check(_native.lib().bk_init(dev), "bk_init")
-            _initialized_device = dev
-            _workspace = _Buffer(_native.lib().bk_reduce_workspace_bytes())
-            _scalar_out = _Buffer(256)
-    return _initialized_device  # type: ignore[return-value]
+        if _driver is None:
+            d = make_driver()
+            d.init(int(os.environ.get("BEE_DEVICE", "0")) if device is None else int(device))
+            _driver = d
+    return _driver.device
+
+
+def driver():
+    if _driver is None:
+        init()
+    return _driver
+
+
+def driver_name() -> str:
+    return driver().name
 
 
 def is_initialized() -> bool:
-    return _initialized_device is not None
+    return _driver is not None
 
 
 def synchronize() -> None:
-    if is_initialized():
-        check(_native.lib().bk_sync(_stream), "bk_sync")
+    if _driver is not None:
+        _driver.sync()
 
 
 def memory_stats() -> dict:
-    stats = (ctypes.c_int64 * 4)()
-    check(_native.lib().bk_memory_stats(stats), "bk_memory_stats")
-    return {"in_use": stats[0], "cached": stats[1], "peak": stats[2], "quota": stats[3]}
+    return driver().memory_stats()
 
 
 def set_quota(nbytes: int) -> None:
-    check(_native.lib().bk_set_quota(int(nbytes)), "bk_set_quota")
+    driver().set_quota(int(nbytes))
 
 
 def empty_cache() -> None:
-    check(_native.lib().bk_empty_cache(), "bk_empty_cache")
+    driver().empty_cache()
 
 
 def device_info() -> dict:
-    init()
-    info = (ctypes.c_int64 * 5)()
-    name = ctypes.create_string_buffer(64)
-    check(_native.lib().bk_device_info(info, name, 64), "bk_device_info")
-    return {
-        "arch": name.value.decode(),
-        "compute_units": info[0],
-        "total_bytes": info[1],
-        "free_bytes": info[2],
-        "clock_khz": info[3],
-        "lds_bytes_per_cu": info[4],
-    }
+    return driver().device_info()
 
 
 class _Buffer:
-    """Owns one device allocation from the caching, quota-checked allocator."""
+    """Owns one device allocation (pointer or broker handle)."""
 
-    __slots__ = ("ptr", "nbytes", "_owner", "__weakref__")
+    __slots__ = ("ptr", "nbytes", "_owner", "_drv", "__weakref__")
 
     def __init__(self, nbytes: int, ptr: Optional[int] = None, owner: Any = None) -> None:
         self.nbytes = int(nbytes)
         self._owner = owner
-        if ptr is not None:
-            self.ptr = int(ptr)
-            return
-        init()
-        out = ctypes.c_void_p()
-        check(_native.lib().bk_malloc(ctypes.byref(out), max(self.nbytes, 1)), "bk_malloc")
-        self.ptr = int(out.value or 0)
+        self._drv = driver()
+        self.ptr = int(ptr) if ptr is not None else self._drv.malloc(max(self.nbytes, 1))
 
     def __del__(self) -> None:
-        if self._owner is None and getattr(self, "ptr", 0) and _native.is_loaded():
+        if self._owner is None and getattr(self, "ptr", 0):
             try:
-                _native.lib().bk_free(ctypes.c_void_p(self.ptr))
+                self._drv.free(self.ptr)
             except Exception:
                 pass
 
@@ -155,7 +140,6 @@ class DeviceArray:
             buffer = _Buffer(self.nbytes)
         self._buf = buffer
 
-    # ---- basic properties ----------------------------------------------------
     @property
     def size(self) -> int:
         return int(math.prod(self.shape)) if self.shape else 1
@@ -177,6 +161,10 @@ class DeviceArray:
         self._materialize()
         return self._buf.ptr  # type: ignore[union-attr]
 
+    @property
+    def code(self) -> int:
+        return DTYPE_CODES[self.dtype]
+
     def __len__(self) -> int:
         if not self.shape:
             raise TypeError("len() of a 0-d array")
@@ -186,30 +174,24 @@ class DeviceArray:
         kind = "lazy " if self._lazy else ""
         return f"DeviceArray({kind}shape={self.shape}, dtype={self.dtype})"
 
-    # ---- lazy fusion ------------------------------------------------------------
     def _materialize(self) -> "DeviceArray":
         if self._lazy is not None:
             op, src = self._lazy
             self._buf = _Buffer(self.nbytes)
-            check(
-                _native.lib().bk_unary(_UNARY[op], DTYPE_CODES[self.dtype], _vp(src.ptr), _vp(self._buf.ptr), self.size, _stream),
-                f"bk_unary({op})",
-            )
+            driver().unary(_UNARY[op], self.code, src.ptr, self._buf.ptr, self.size)
             self._lazy = None
         if self._transposed:
-            src = self._buf
             rows, cols = self.shape[1], self.shape[0]  # underlying buffer is (rows, cols)
-            out = _Buffer(self.nbytes)
+            src = self._buf
             if self.dtype == "bfloat16":
-                check(_native.lib().bk_transpose_bf16(_vp(src.ptr), _vp(out.ptr), rows, cols, cols, rows, _stream), "transpose")
+                out = _Buffer(self.nbytes)
+                driver().transpose(src.ptr, out.ptr, rows, cols, cols, rows)
             else:
-                host = _download(src, (rows, cols), self.dtype)
-                out = _upload(np.ascontiguousarray(host.T), self.dtype)
+                out = _upload(np.ascontiguousarray(_download(src, (rows, cols), self.dtype).T), self.dtype)
             self._buf = out
             self._transposed = False
         return self
 
-    # ---- host transfer ------------------------------------------------------------
     def numpy(self) -> np.ndarray:
         self._materialize()
         return _download(self._buf, self.shape, self.dtype)
@@ -229,7 +211,6 @@ class DeviceArray:
     def __float__(self) -> float:
         return float(self.item())
 
-    # ---- shape ---------------------------------------------------------------------
     def reshape(self, *shape) -> "DeviceArray":
         if len(shape) == 1 and isinstance(shape[0], (tuple, list)):
             shape = tuple(shape[0])
@@ -255,16 +236,12 @@ class DeviceArray:
             return self.copy()
         self._materialize()
         out = DeviceArray(self.shape, dt)
-        check(
-            _native.lib().bk_cast(DTYPE_CODES[self.dtype], DTYPE_CODES[dt], _vp(self.ptr), _vp(out.ptr), self.size, _stream),
-            "bk_cast",
-        )
+        driver().cast(self.code, out.code, self.ptr, out.ptr, self.size)
         return out
 
     def copy(self) -> "DeviceArray":
         return _unary("copy", self)
 
-    # ---- reductions ----------------------------------------------------------------
     def sum(self):
         return sum(self)
 
@@ -277,7 +254,6 @@ class DeviceArray:
     def min(self):
         return _reduce("min", self)
 
-    # ---- operators -----------------------------------------------------------------
     def __add__(self, o): return _binary("add", self, o)
     def __radd__(self, o): return _binary("add", self, o)
     def __sub__(self, o): return _binary("subtract", self, o)
@@ -298,18 +274,13 @@ class DeviceArray:
     def __matmul__(self, o): return matmul(self, o)
 
 
-def _vp(p: int) -> ctypes.c_void_p:
-    return ctypes.c_void_p(p)
-
-
 def _np_view_dtype(dtype: str):
     return np.uint16 if dtype == "bfloat16" else _NP_DTYPES[dtype]
 
 
 def _download(buf: _Buffer, shape: Shape, dtype: str) -> np.ndarray:
     host = np.empty(shape, dtype=_np_view_dtype(dtype))
-    if host.nbytes:
-        check(_native.lib().bk_memcpy(host.ctypes.data, _vp(buf.ptr), host.nbytes, 2, _stream), "download")
+    driver().d2h(buf.ptr, host)
     if dtype == "bfloat16":
         return (host.astype(np.uint32) << 16).view(np.float32)
     return host
@@ -318,8 +289,7 @@ def _download(buf: _Buffer, shape: Shape, dtype: str) -> np.ndarray:
 def _upload(host: np.ndarray, dtype: str) -> _Buffer:
     host = np.ascontiguousarray(host)
     buf = _Buffer(host.nbytes)
-    if host.nbytes:
-        check(_native.lib().bk_memcpy(_vp(buf.ptr), host.ctypes.data, host.nbytes, 1, _stream), "upload")
+    driver().h2d(buf.ptr, host)
     return buf
 
 
@@ -342,14 +312,13 @@ def empty(shape, dtype="float64") -> DeviceArray:
 
 def full(shape, value: float, dtype="float64") -> DeviceArray:
     a = empty(shape, dtype)
-    dt = a.dtype
-    if dt == "float64":
+    if a.dtype == "float64":
         pattern, width = int(np.array(value, np.float64).view(np.uint64)), 8
-    elif dt == "float32":
+    elif a.dtype == "float32":
         pattern, width = int(np.array(value, np.float32).view(np.uint32)), 4
     else:
         pattern, width = int(_f32_to_bf16_bits(np.array([value], np.float32))[0]), 2
-    check(_native.lib().bk_fill(_vp(a.ptr), a.nbytes, pattern, width, _stream), "bk_fill")
+    driver().fill(a.ptr, a.nbytes, pattern, width)
     return a
 
 
@@ -385,13 +354,18 @@ def _is_torch_tensor(x) -> bool:
 
 
 def from_torch(t) -> DeviceArray:
-    """Zero-copy view of a contiguous HIP torch tensor (keeps it alive)."""
-    if not t.is_cuda:
-        return asarray(t.numpy())
-    t = t.contiguous()
+    """Zero-copy view of a contiguous HIP torch tensor when this process owns
+    the HIP context; a host copy in broker mode."""
     dt = normalize_dtype(str(t.dtype).replace("torch.", ""))
-    init()
-    return DeviceArray(tuple(t.shape), dt, buffer=_Buffer(t.numel() * t.element_size(), ptr=t.data_ptr(), owner=t))
+    if t.is_cuda and driver().name == "native":
+        t = t.contiguous()
+        return DeviceArray(tuple(t.shape), dt, buffer=_Buffer(t.numel() * t.element_size(), ptr=t.data_ptr(), owner=t))
+    host = t.detach().cpu()
+    if dt == "bfloat16":
+        import torch
+
+        return asarray(host.to(torch.float32).numpy(), "bfloat16")
+    return asarray(host.numpy(), dt)
 
 
 def to_torch(a: DeviceArray):
@@ -405,15 +379,13 @@ def to_torch(a: DeviceArray):
 # ---- elementwise / reductions ------------------------------------------------------
 
 def _as_operand(x) -> DeviceArray:
-    if isinstance(x, DeviceArray):
-        return x
-    return asarray(x)
+    return x if isinstance(x, DeviceArray) else asarray(x)
 
 
 def _unary(op: str, x) -> DeviceArray:
     x = _as_operand(x)._materialize()
     out = DeviceArray(x.shape, x.dtype)
-    check(_native.lib().bk_unary(_UNARY[op], DTYPE_CODES[x.dtype], _vp(x.ptr), _vp(out.ptr), x.size, _stream), f"bk_unary({op})")
+    driver().unary(_UNARY[op], x.code, x.ptr, out.ptr, x.size)
     return out
 
 
@@ -427,11 +399,7 @@ def _binary(op: str, a, b, reversed_: bool = False) -> DeviceArray:
     a = _as_operand(a)._materialize()
     if isinstance(b, (int, float, np.floating, np.integer)):
         out = DeviceArray(a.shape, a.dtype)
-        mode = 2 if reversed_ else 1
-        check(
-            _native.lib().bk_binary(_BINARY[op], DTYPE_CODES[a.dtype], mode, _vp(a.ptr), None, float(b), _vp(out.ptr), a.size, _stream),
-            f"bk_binary({op})",
-        )
+        driver().binary(_BINARY[op], a.code, 2 if reversed_ else 1, a.ptr, 0, float(b), out.ptr, a.size)
         return out
     b = _as_operand(b)._materialize()
     if b.shape != a.shape or b.dtype != a.dtype:
@@ -441,30 +409,18 @@ def _binary(op: str, a, b, reversed_: bool = False) -> DeviceArray:
     if reversed_:
         a, b = b, a
     out = DeviceArray(a.shape, a.dtype)
-    check(
-        _native.lib().bk_binary(_BINARY[op], DTYPE_CODES[a.dtype], 0, _vp(a.ptr), _vp(b.ptr), 0.0, _vp(out.ptr), a.size, _stream),
-        f"bk_binary({op})",
-    )
+    driver().binary(_BINARY[op], a.code, 0, a.ptr, b.ptr, 0.0, out.ptr, a.size)
     return out
 
 
 def _reduce(op: str, x: DeviceArray, y: Optional[DeviceArray] = None) -> np.float64:
-    init()
-    lib = _native.lib()
-    b_ptr = _vp(y.ptr) if y is not None else None
-    check(
-        lib.bk_reduce(_REDUCE[op], DTYPE_CODES[x.dtype], _vp(x.ptr), b_ptr, x.size, _vp(_workspace.ptr), _vp(_scalar_out.ptr), _stream),
-        f"bk_reduce({op})",
-    )
-    out = np.zeros(1, np.float64)
-    check(lib.bk_memcpy(out.ctypes.data, _vp(_scalar_out.ptr), 8, 2, _stream), "reduce readback")
-    return np.float64(out[0])
+    return np.float64(driver().reduce(_REDUCE[op], x.code, x.ptr, y.ptr if y is not None else 0, x.size))
 
 
 def sum(x) -> np.float64:  # noqa: A001 - numpy-compatible name
     x = _as_operand(x)
     if x._lazy is not None and x._lazy[0] == "square":
-        return _reduce("square_sum", x._lazy[1])  # fused: x never materialised
+        return _reduce("square_sum", x._lazy[1])  # fused: x**2 never materialised
     return _reduce("sum", x._materialize())
 
 
@@ -477,7 +433,7 @@ def mean(x) -> np.float64:
     return sum(x) / x.size
 
 
-def dot(a, b) -> np.float64:
+def dot(a, b):
     a, b = _as_operand(a)._materialize(), _as_operand(b)._materialize()
     if a.ndim == 2 or b.ndim == 2:
         return matmul(a, b)
@@ -493,6 +449,7 @@ def amin(x): return _reduce("min", _as_operand(x)._materialize())
 def _make_unary(name):
     def fn(x):
         return _unary(name, x)
+
     fn.__name__ = name
     return fn
 
@@ -523,9 +480,9 @@ def power(a, b): return _binary("power", a, b)
 def matmul(a, b, out_dtype: str = "bfloat16") -> DeviceArray:
     """C = A @ B on the bf16 MFMA GEMM (f32 accumulate).
 
-    Operands are converted to bf16 if needed; ``b`` is consumed as Bt[N, K]
-    (K-contiguous), so a plain row-major ``b`` is transposed once on device
-    (~1 % of a 4096³ GEMM) and ``b.T`` views are used directly.
+    ``b`` is consumed as Bt[N, K] (K-contiguous): ``b.T`` views of a
+    row-major [N, K] buffer are used as is; a plain row-major ``b`` is
+    transposed once on device (~1 % of a 4096^3 GEMM).
     """
     a = _as_operand(a)
     b = _as_operand(b)
@@ -537,23 +494,19 @@ def matmul(a, b, out_dtype: str = "bfloat16") -> DeviceArray:
         a = a.astype("bfloat16")
     a._materialize()
     if b._transposed and b.dtype == "bfloat16" and b._lazy is None:
-        bt_buf = b._buf  # underlying buffer already is Bt[N, K]
+        bt_ptr = b._buf.ptr  # the underlying buffer already is Bt[N, K]
+        keep = b
     else:
         if b.dtype != "bfloat16":
             b = b.astype("bfloat16")
         b._materialize()
-        bt = DeviceArray((N, K), "bfloat16")
-        check(_native.lib().bk_transpose_bf16(_vp(b.ptr), _vp(bt.ptr), K, N, N, K, _stream), "transpose")
-        bt_buf = bt._buf
-        b = bt
+        keep = DeviceArray((N, K), "bfloat16")
+        driver().transpose(b.ptr, keep.ptr, K, N, N, K)
+        bt_ptr = keep.ptr
     out_dtype = normalize_dtype(out_dtype)
     c = DeviceArray((M, N), out_dtype)
-    check(
-        _native.lib().bk_gemm_bf16_tn(
-            _vp(a.ptr), _vp(bt_buf.ptr), _vp(c.ptr), M, N, K, K, K, N, 1.0, 0.0, DTYPE_CODES[out_dtype], _stream
-        ),
-        "bk_gemm_bf16_tn",
-    )
+    driver().gemm(a.ptr, bt_ptr, c.ptr, M, N, K, K, K, N, 1.0, 0.0, DTYPE_CODES[out_dtype])
+    del keep
     return c
 
 
@@ -561,13 +514,9 @@ def gemm_bf16_tn(a: DeviceArray, bt: DeviceArray, out_dtype: str = "bfloat16", a
     """Raw C = alpha * A . Bt^T with both operands already bf16 [M,K] / [N,K]."""
     M, K = a.shape
     N = bt.shape[0]
+    out_dtype = normalize_dtype(out_dtype)
     c = DeviceArray((M, N), out_dtype)
-    check(
-        _native.lib().bk_gemm_bf16_tn(
-            _vp(a.ptr), _vp(bt.ptr), _vp(c.ptr), M, N, K, K, K, N, float(alpha), 0.0, DTYPE_CODES[normalize_dtype(out_dtype)], _stream
-        ),
-        "bk_gemm_bf16_tn",
-    )
+    driver().gemm(a.ptr, bt.ptr, c.ptr, M, N, K, K, K, N, float(alpha), 0.0, DTYPE_CODES[out_dtype])
     return c
 
 
@@ -596,20 +545,18 @@ class Generator:
     def rand(self, *shape, dtype="float64") -> DeviceArray:
         return self.uniform(0.0, 1.0, shape or (1,), dtype)
 
-    def uniform(self, low=0.0, high=1.0, size=None, dtype="float64") -> DeviceArray:
+    def _draw(self, kind: int, a: float, b: float, size, dtype) -> DeviceArray:
         shape = _shape_of(size)
-        out = DeviceArray(shape, dtype)
-        per = 2 if out.dtype == "float64" else 4
-        if out.dtype == "bfloat16":
-            tmp = self.uniform(low, high, shape, "float32")
-            return tmp.astype("bfloat16")
-        check(
-            _native.lib().bk_rand_uniform(
-                _vp(out.ptr), out.size, DTYPE_CODES[out.dtype], self._seed, self._advance(out.size, per), float(low), float(high), _stream
-            ),
-            "bk_rand_uniform",
-        )
+        dt = normalize_dtype(dtype)
+        if dt == "bfloat16":
+            return self._draw(kind, a, b, shape, "float32").astype("bfloat16")
+        out = DeviceArray(shape, dt)
+        per = 2 if dt == "float64" else 4
+        driver().rand(kind, out.ptr, out.size, out.code, self._seed, self._advance(out.size, per), float(a), float(b))
         return out
+
+    def uniform(self, low=0.0, high=1.0, size=None, dtype="float64") -> DeviceArray:
+        return self._draw(0, low, high, size, dtype)
 
     def randn(self, *shape, dtype="float64") -> DeviceArray:
         return self.normal(0.0, 1.0, shape or (1,), dtype)
@@ -618,18 +565,7 @@ class Generator:
         return self.normal(0.0, 1.0, size, dtype)
 
     def normal(self, loc=0.0, scale=1.0, size=None, dtype="float64") -> DeviceArray:
-        shape = _shape_of(size)
-        out = DeviceArray(shape, dtype)
-        if out.dtype == "bfloat16":
-            return self.normal(loc, scale, shape, "float32").astype("bfloat16")
-        per = 2 if out.dtype == "float64" else 4
-        check(
-            _native.lib().bk_rand_normal(
-                _vp(out.ptr), out.size, DTYPE_CODES[out.dtype], self._seed, self._advance(out.size, per), float(loc), float(scale), _stream
-            ),
-            "bk_rand_normal",
-        )
-        return out
+        return self._draw(1, loc, scale, size, dtype)
 
 
 def _shape_of(size) -> Shape:
@@ -668,20 +604,12 @@ random = _RandomModule()
 
 
 class Timer:
-    """Device-side timing with HIP events: ``with Timer() as t: ...; t.ms``."""
+    """Device timing: HIP events (native) or synced wall clock (broker)."""
 
     def __enter__(self):
-        init()
-        s, e = ctypes.c_void_p(), ctypes.c_void_p()
-        check(_native.lib().bk_event_pair_create(ctypes.byref(s), ctypes.byref(e)), "events")
-        self._s, self._e = s, e
-        check(_native.lib().bk_event_record(s, _stream), "event record")
+        self._tok = driver().timer_start()
         return self
 
     def __exit__(self, *exc):
-        lib = _native.lib()
-        check(lib.bk_event_record(self._e, _stream), "event record")
-        self.ms = float(lib.bk_event_elapsed_ms(self._s, self._e))
-        lib.bk_event_destroy(self._s)
-        lib.bk_event_destroy(self._e)
+        self.ms = driver().timer_stop(self._tok)
         return False

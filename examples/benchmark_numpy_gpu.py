@@ -1,0 +1,26 @@
+# benchmark-numpy payload, MI355X edition: the reference's workload
+# (examples/benchmark-numpy.py: 1e8 float64 uniform draws, square, sum) on
+# the sandbox's pinned GPU through the hand-written beekern kernels, plus the
+# 4096^3 bf16 GEMM of BASELINE config 3.  Same printed lines as the original.
+import time
+
+import beekern as bk
+
+
+def gpu_intensive_computation():
+    n = 10**8
+    x = bk.random.rand(n)              # Philox4x32-10, f64, stays in HBM
+    result = bk.sum(bk.square(x))      # fused square+sum: one HBM pass
+    a = bk.random.uniform(-1, 1, (4096, 4096), dtype="bfloat16")
+    b = bk.random.uniform(-1, 1, (4096, 4096), dtype="bfloat16")
+    c = bk.matmul(a, b.T)              # MFMA bf16 GEMM, f32 accumulate
+    checksum = bk.sum(c)
+    return result, checksum
+
+
+start_time = time.time()
+result, checksum = gpu_intensive_computation()
+end_time = time.time()
+print("Result:", result)
+print("GEMM checksum:", checksum)
+print("Execution Time:", end_time - start_time, "seconds")

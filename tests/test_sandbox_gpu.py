@@ -1,0 +1,108 @@
+"""GPU-pinned sandboxes on a real MI355X: the service path end to end."""
+
+import tempfile
+
+import pytest
+
+from .harness import ServiceHarness, ensure_native_executor
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gsvc():
+    ensure_native_executor()
+    h = ServiceHarness(tempfile.mkdtemp(prefix="bee-gpu-"), gpu_ids=[0], workers_per_gpu_target=2, default_timeout=120.0)
+    h.start()
+    yield h
+    h.stop()
+
+
+def run(h, code, **kw):
+    return h.call(h.ctx.code_executor.execute(source_code=code, **kw), timeout=300)
+
+
+def test_payload_runs_on_pinned_gpu(gsvc):
+    import os
+
+    src = open(os.path.join(os.path.dirname(__file__), "..", "examples", "benchmark_numpy_gpu.py")).read()
+    r = run(gsvc, src)
+    assert r.exit_code == 0, r.stderr
+    val = float(r.stdout.split("Result:")[1].split()[0])
+    assert abs(val - 1e8 / 3) < 5e4
+    assert r.gpu_ids == [0]
+
+
+def test_sandbox_sees_only_its_gpu_and_is_warm(gsvc):
+    code = (
+        "import os, beekern as bk\n"
+        "print(os.environ['HIP_VISIBLE_DEVICES'], bk.is_initialized(), bk.device_info()['arch'].split(':')[0])\n"
+    )
+    r = run(gsvc, code)
+    assert r.exit_code == 0, r.stderr
+    assert r.stdout.split() == ["0", "True", "gfx950"]
+
+
+def test_light_and_direct_sandboxes(gsvc):
+    light = run(gsvc, "import beekern as bk\nbk.init()\nprint(bk.driver_name())")
+    assert light.stdout.strip() == "broker", light.stderr
+    direct = run(gsvc, "import torch, beekern as bk\nbk.init()\nprint(bk.driver_name(), torch.cuda.is_initialized())")
+    assert direct.stdout.split()[0] == "native", direct.stderr
+
+
+def test_broker_rejects_out_of_bounds(gsvc):
+    code = (
+        "from bee_code_interpreter_fs_amd.ops.array import driver\n"
+        "import beekern as bk\n"
+        "x = bk.empty((16,), 'float64')\n"
+        "try:\n"
+        "    driver().unary(0, 1, x.ptr, x.ptr, 1 << 30)\n"
+        "    print('unchecked')\n"
+        "except bk.BeekernError as e:\n"
+        "    print('rejected')\n"
+        "try:\n"
+        "    driver().unary(0, 1, 987654, x.ptr, 4)\n"
+        "    print('unchecked')\n"
+        "except bk.BeekernError as e:\n"
+        "    print('rejected')\n"
+    )
+    r = run(gsvc, code)
+    assert r.stdout.split() == ["rejected", "rejected"], (r.stdout, r.stderr)
+
+
+def test_torch_inside_sandbox(gsvc):
+    code = (
+        "import torch\n"
+        "x = torch.randn(1024, 1024, device='cuda')\n"
+        "print(torch.cuda.device_count(), float((x @ x.T).diagonal().mean()) > 0)\n"
+    )
+    r = run(gsvc, code)
+    assert r.exit_code == 0, r.stderr
+    assert r.stdout.split() == ["1", "True"]
+
+
+def test_hbm_quota_enforced_in_sandbox(gsvc):
+    code = (
+        "import beekern as bk\n"
+        "try:\n"
+        "    x = bk.empty((4 << 30,), 'float64')\n"
+        "    print('allocated')\n"
+        "except bk.QuotaExceeded as e:\n"
+        "    print('quota', e)\n"
+    )
+    r = run(gsvc, code, hbm_bytes=1 << 30)  # 1 GiB quota, 32 GiB request
+    assert r.exit_code == 0, r.stderr
+    assert r.stdout.startswith("quota"), r.stdout
+
+
+def test_concurrent_gpu_executions(gsvc):
+    import asyncio
+
+    code = "import beekern as bk\nprint(round(float(bk.sum(bk.square(bk.random.rand(10**7)))) / 1e7, 2))"
+
+    async def many():
+        ex = gsvc.ctx.code_executor
+        return await asyncio.gather(*(ex.execute(source_code=code) for _ in range(8)))
+
+    rs = gsvc.call(many(), timeout=300)
+    assert all(r.exit_code == 0 and r.stdout.strip() == "0.33" for r in rs), [(r.stdout, r.stderr[-200:]) for r in rs]
