@@ -90,6 +90,8 @@ class Config:
     light_workers_per_gpu_target: int = 8
     # run the per-GPU kernel broker in the executor daemon
     broker_enabled: bool = True
+    # zygote processes forking light sandboxes per GPU (fork parallelism)
+    light_zygotes_per_gpu: int = 2
     # concurrent executions admitted per GPU pool (others queue)
     max_inflight_per_gpu: int = 16
     # per-sandbox HBM quota in bytes (0 = 288 GB / max_inflight_per_gpu minus reserve)

@@ -32,6 +32,7 @@ import traceback
 from typing import Optional
 
 SANDBOX_SITE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sandbox_site")
+_STAMPS: dict = {}  # phase timestamps reported to the executor
 
 
 def _send(sock: socket.socket, msg: dict) -> None:
@@ -127,6 +128,7 @@ def run_script(script: str, argv, workspace: str, runtime_packages: str) -> int:
     except OSError:
         pass
     code = 0
+    _STAMPS["script_start"] = time.monotonic() * 1e3
     try:
         runpy.run_path(script, run_name="__main__")
     except SystemExit as e:
@@ -145,11 +147,14 @@ def run_script(script: str, argv, workspace: str, runtime_packages: str) -> int:
     return code
 
 
-def _finish(code: int) -> None:
+def _finish(code: int, timing_path: Optional[str] = None, sock: Optional[socket.socket] = None) -> None:
+    _STAMPS["script_end"] = time.monotonic() * 1e3
     try:
         import atexit
 
-        atexit._run_exitfuncs()
+        atexit._run_exitfuncs()  # only the user's: the zygote cleared its own
+        if "logging" in sys.modules:
+            sys.modules["logging"].shutdown()
     except BaseException:
         pass
     for stream in (sys.stdout, sys.stderr):
@@ -157,7 +162,22 @@ def _finish(code: int) -> None:
             stream.flush()
         except Exception:
             pass
-    os._exit(code & 0xFF if code >= 0 else 1)
+    _STAMPS["exit"] = time.monotonic() * 1e3
+    status = code & 0xFF if code >= 0 else 1
+    if timing_path:
+        try:  # CLOCK_MONOTONIC ms, the executor's clock too
+            with open(timing_path, "w") as fh:
+                json.dump(_STAMPS, fh)
+        except OSError:
+            pass
+    if sock is not None:
+        # outputs are flushed: the executor can answer now and reap this
+        # process (and anything it left behind) off the request path
+        try:
+            _send(sock, {"op": "done", "code": status})
+        except OSError:
+            pass
+    os._exit(status)
 
 
 def worker_main(spawn: dict) -> None:
@@ -179,6 +199,7 @@ def worker_main(spawn: dict) -> None:
         job = _recv_line(sock)
         if job is None or job.get("op") != "run":
             os._exit(0)
+        _STAMPS["recv"] = time.monotonic() * 1e3
         for k, v in (job.get("env") or {}).items():
             os.environ[k] = str(v)
         quota = int(job.get("hbm_quota") or 0)
@@ -196,4 +217,4 @@ def worker_main(spawn: dict) -> None:
         finally:
             os._exit(70)
     code = run_script(job["script"], job.get("argv") or [], cwd, os.environ.get("BEE_RUNTIME_PACKAGES", ""))
-    _finish(code)
+    _finish(code, os.path.join(os.path.dirname(job["stdout"]), "timing.json"), sock)

@@ -50,8 +50,10 @@ class ExecutorProcess:
         use_interposer: bool = True,
         light_target: int = 0,
         broker: bool = False,
+        light_zygotes: int = 2,
     ) -> None:
         self.light_target = light_target
+        self.light_zygotes = light_zygotes
         self.broker = broker
         self.name = name
         self.sandbox_root = os.path.abspath(sandbox_root)
@@ -92,7 +94,7 @@ class ExecutorProcess:
         ]
         lib = os.path.join(ROOT, "bee_code_interpreter_fs_amd", "ops", "lib", "libbeekern.so")
         if self.broker and self.gpus and os.path.exists(lib):
-            cmd += ["--broker-lib", lib, "--light-target", str(self.light_target)]
+            cmd += ["--broker-lib", lib, "--light-target", str(self.light_target), "--light-zygotes", str(self.light_zygotes)]
         interposer = hbm_interposer_path()
         if self.use_interposer and self.gpus and os.path.exists(interposer):
             cmd += ["--preload", interposer]

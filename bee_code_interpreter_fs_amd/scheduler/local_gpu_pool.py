@@ -119,6 +119,7 @@ class LocalGpuPoolBackend(CodeExecutor):
             extra_env={"BEE_WHEELHOUSE": c.wheelhouse} if c.wheelhouse else None,
             light_target=c.light_workers_per_gpu_target,
             broker=c.broker_enabled,
+            light_zygotes=c.light_zygotes_per_gpu,
         )
 
     async def wait_ready(self, timeout: float = 300.0) -> None:

@@ -193,6 +193,12 @@ def main():
             out["first_error"] = all_err[0][:400]
         if gang is not None:
             out["gang_allreduce"] = gang
+        try:
+            st = service.call(service.ctx.code_executor.status(), timeout=30)
+            keys = ("mean_warm_ms", "mean_worker_warm_ms", "mean_fork_ms", "mean_acquire_ms", "executions")
+            out["executors"] = [{k: round(s["executor"].get(k, 0), 3) for k in keys} for s in st["slots"]]
+        except Exception as e:  # noqa: BLE001
+            out["executors"] = repr(e)[:200]
         print(json.dumps(out), flush=True)
         service.stop()
     if world > 1:

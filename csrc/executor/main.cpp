@@ -115,6 +115,8 @@ int main(int argc, char** argv) {
     else if (a == "--die-with-parent") die_with_parent = val() != "0";
     else if (a == "--broker-lib") cfg.broker_lib = val();
     else if (a == "--light-target") cfg.light_target = atoi(val().c_str());
+    else if (a == "--light-zygotes") cfg.light_zygotes = atoi(val().c_str());
+    else if (a == "--light-preload") cfg.light_preload = val();
     else if (a == "--runtime-packages") cfg.pod_runtime_packages = val();
     else if (a == "-h" || a == "--help") {
       usage();

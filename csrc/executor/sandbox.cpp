@@ -93,9 +93,17 @@ bool SandboxPool::start(std::string* err) {
     return false;
   }
   // the zygote is forked+exec'd BEFORE this process touches HIP (broker init)
-  if (!start_zygote(err)) return false;
-  if (!cfg_.broker_lib.empty() && !cfg_.gpus.empty() && !cfg_.pod_mode) {
-    broker_ = std::make_unique<KernelBroker>(join_path(cfg_.run_dir, "broker-" + std::to_string(getpid()) + ".sock"),
+  const bool want_broker = !cfg_.broker_lib.empty() && !cfg_.gpus.empty() && !cfg_.pod_mode;
+  const int nz = 1 + (want_broker ? std::max(1, cfg_.light_zygotes) : 0);
+  for (int i = 0; i < nz; ++i) {
+    auto z = std::make_unique<Zygote>();
+    z->index = i;
+    z->kind = i == 0 ? kDirect : kLight;
+    if (!start_zygote(z.get(), err)) return false;
+    zygotes_.push_back(std::move(z));
+  }
+  if (want_broker) {
+    broker_ =std::make_unique<KernelBroker>(join_path(cfg_.run_dir, "broker-" + std::to_string(getpid()) + ".sock"),
                                              cfg_.broker_lib, [this](pid_t p) { return peer_quota(p); });
     if (!broker_->start(err)) {
       BEE_ERROR("kernel broker disabled: %s", err->c_str());
@@ -120,28 +128,31 @@ void SandboxPool::stop() {
       if (kv.second->pid > 0) kill(-kv.second->pid, SIGKILL);
     }
   }
-  if (zygote_pid_ > 0) {
-    kill(zygote_pid_, SIGTERM);
-    for (int i = 0; i < 50; ++i) {
-      if (waitpid(zygote_pid_, nullptr, WNOHANG) == zygote_pid_) break;
-      usleep(20000);
+  for (auto& z : zygotes_) {
+    if (z->pid > 0) {
+      kill(z->pid, SIGTERM);
+      for (int i = 0; i < 50; ++i) {
+        if (waitpid(z->pid, nullptr, WNOHANG) == z->pid) break;
+        usleep(20000);
+      }
+      kill(z->pid, SIGKILL);
+      waitpid(z->pid, nullptr, WNOHANG);
     }
-    kill(zygote_pid_, SIGKILL);
-    waitpid(zygote_pid_, nullptr, WNOHANG);
+    if (z->fd >= 0) shutdown(z->fd, SHUT_RDWR);
   }
-  if (zygote_fd_ >= 0) shutdown(zygote_fd_, SHUT_RDWR);
   if (worker_listen_fd_ >= 0) shutdown(worker_listen_fd_, SHUT_RDWR);
   unlink(worker_sock_path_.c_str());
   cv_.notify_all();
   cleanup_cv_.notify_all();
-  if (zygote_thread_.joinable()) zygote_thread_.join();
+  for (auto& z : zygotes_)
+    if (z->thread.joinable()) z->thread.join();
   if (acceptor_thread_.joinable()) acceptor_thread_.join();
   if (cleanup_thread_.joinable()) cleanup_thread_.join();
 }
 
 // ---- zygote ---------------------------------------------------------------------
 
-bool SandboxPool::start_zygote(std::string* err) {
+bool SandboxPool::start_zygote(Zygote* z, std::string* err) {
   int sv[2];
   if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv) != 0) {
     *err = std::string("socketpair: ") + strerror(errno);
@@ -152,12 +163,16 @@ bool SandboxPool::start_zygote(std::string* err) {
   for (char** e = environ; *e; ++e) {
     std::string kv = *e;
     if (kv.rfind("BEE_ZYGOTE_FD=", 0) == 0 || kv.rfind("BEE_WORKER_SOCK=", 0) == 0) continue;
+    if (kv.rfind("BEE_ZYGOTE_KIND=", 0) == 0) continue;
+    if (z->kind == kLight && kv.rfind("BEE_PRELOAD=", 0) == 0) continue;
     if (!cfg_.pythonpath.empty() && kv.rfind("PYTHONPATH=", 0) == 0) continue;
     if (!cfg_.zygote_preload.empty() && kv.rfind("LD_PRELOAD=", 0) == 0) continue;
     env_store.push_back(kv);
   }
   env_store.push_back("BEE_ZYGOTE_FD=" + std::to_string(sv[1]));
   env_store.push_back("BEE_WORKER_SOCK=" + worker_sock_path_);
+  env_store.push_back(std::string("BEE_ZYGOTE_KIND=") + (z->kind == kLight ? "light" : "direct"));
+  if (z->kind == kLight) env_store.push_back("BEE_PRELOAD=" + cfg_.light_preload);
   if (!cfg_.pythonpath.empty()) {
     const char* old = getenv("PYTHONPATH");
     env_store.push_back("PYTHONPATH=" + cfg_.pythonpath + (old && *old ? std::string(":") + old : ""));
@@ -187,24 +202,40 @@ bool SandboxPool::start_zygote(std::string* err) {
     _exit(127);
   }
   close(sv[1]);
-  zygote_pid_ = pid;
-  zygote_fd_ = sv[0];
-  zygote_alive_ = true;
-  if (zygote_thread_.joinable()) zygote_thread_.detach();
-  zygote_thread_ = std::thread([this] { zygote_reader(); });
-  BEE_INFO("zygote started pid=%d (%s -m %s), gpus='%s'", pid, cfg_.python.c_str(), cfg_.zygote_module.c_str(),
-           cfg_.gpus.c_str());
+  z->pid = pid;
+  z->fd = sv[0];
+  z->alive = true;
+  if (z->thread.joinable()) z->thread.detach();
+  z->thread = std::thread([this, z] { zygote_reader(z); });
+  BEE_INFO("zygote %d (%s) started pid=%d (%s -m %s), gpus='%s'", z->index, z->kind == kLight ? "light" : "direct",
+           pid, cfg_.python.c_str(), cfg_.zygote_module.c_str(), cfg_.gpus.c_str());
   return true;
 }
 
-void SandboxPool::send_zygote(const Json& msg) {
-  std::lock_guard<std::mutex> lk(zygote_write_mu_);
-  if (zygote_fd_ < 0 || !send_line(zygote_fd_, msg)) BEE_WARN("zygote write failed");
+void SandboxPool::send_zygote(Zygote* z, const Json& msg) {
+  std::lock_guard<std::mutex> lk(z->write_mu);
+  if (z->fd < 0 || !send_line(z->fd, msg)) BEE_WARN("zygote %d write failed", z->index);
 }
 
-void SandboxPool::zygote_reader() {
+Zygote* SandboxPool::pick_zygote(int kind) {
+  // direct sandboxes come from zygote 0 (torch preloaded); light ones are
+  // spread over the light zygotes so forks run in parallel
+  std::vector<Zygote*> light;
+  for (auto& z : zygotes_)
+    if (z->kind == kLight && z->alive) light.push_back(z.get());
+  if (kind == kLight && !light.empty()) return light[rr_++ % light.size()];
+  return zygotes_[0].get();
+}
+
+bool SandboxPool::any_zygote_alive() const {
+  for (auto& z : zygotes_)
+    if (z->alive) return true;
+  return false;
+}
+
+void SandboxPool::zygote_reader(Zygote* z) {
   std::string buf, line;
-  const int fd = zygote_fd_;
+  const int fd = z->fd;
   while (read_line(fd, buf, &line)) {
     Json m;
     try {
@@ -224,6 +255,8 @@ void SandboxPool::zygote_reader() {
         it->second->pid = (pid_t)m["pid"].as_int();
         by_pid_[it->second->pid] = it->second;
       }
+      m_fork_ms_sum_ += m["fork_ms"].as_number();
+      m_fork_count_++;
     } else if (op == "spawn_failed") {
       auto it = workers_.find(m["id"].as_string());
       if (it != workers_.end()) {
@@ -232,7 +265,7 @@ void SandboxPool::zygote_reader() {
         w->fail_reason = m["error"].as_string();
         workers_.erase(it);
         if (w->pooled) spawning_[w->kind]--;
-        inflight_spawns_--;
+        if (w->kind == kDirect) inflight_spawns_--;
         m_spawn_failed_++;
         BEE_WARN("spawn of %s failed: %s", w->id.c_str(), w->fail_reason.c_str());
       }
@@ -243,6 +276,7 @@ void SandboxPool::zygote_reader() {
         auto w = it->second;
         by_pid_.erase(it);
         const int sig = (int)m["signal"].as_int();
+        w->t_exit = mono_ms();
         w->exited = true;
         w->term_signal = sig;
         w->exit_code = sig ? -1 : (int)m["code"].as_int();
@@ -251,7 +285,7 @@ void SandboxPool::zygote_reader() {
         if (prev == WorkerState::Spawning || prev == WorkerState::Connected) {
           // died before it became ready
           if (w->pooled) spawning_[w->kind]--;
-          inflight_spawns_--;
+          if (w->kind == kDirect) inflight_spawns_--;
           m_spawn_failed_++;
           workers_.erase(w->id);
           cleanup_dirs_.push_back(w->dir);
@@ -277,40 +311,59 @@ void SandboxPool::zygote_reader() {
     cv_.notify_all();
     cleanup_cv_.notify_all();
   }
-  zygote_alive_ = false;
+  z->alive = false;
   cv_.notify_all();
   if (stopping_) return;
-  BEE_ERROR("zygote channel closed; restarting zygote");
+  BEE_ERROR("zygote %d channel closed; restarting it", z->index);
   int status = 0;
-  if (zygote_pid_ > 0) waitpid(zygote_pid_, &status, 0);
+  if (z->pid > 0) waitpid(z->pid, &status, 0);
   {
     std::lock_guard<std::mutex> lk(mu_);
-    // every worker forked by the dead zygote is unusable (no exit reports)
-    for (auto& kv : workers_) {
-      if (kv.second->pid > 0) kill(-kv.second->pid, SIGKILL);
-      kv.second->exited = true;
-      kv.second->exit_code = -1;
-      kv.second->state = WorkerState::Exited;
+    // spawns still queued for this zygote were never sent: counted in
+    // spawning_ only
+    for (auto it = spawn_queue_.begin(); it != spawn_queue_.end();) {
+      if (it->first->zygote == z->index) {
+        if (it->first->pooled) spawning_[it->first->kind]--;
+        workers_.erase(it->first->id);
+        it = spawn_queue_.erase(it);
+      } else {
+        ++it;
+      }
     }
-    workers_.clear();
-    by_pid_.clear();
-    for (int k = 0; k < 2; ++k) {
-      ready_[k].clear();
-      spawning_[k] = 0;
+    // workers forked by the dead zygote are unusable (nobody reports their exit)
+    std::vector<std::shared_ptr<Worker>> dead;
+    for (auto& kv : workers_)
+      if (kv.second->zygote == z->index) dead.push_back(kv.second);
+    for (auto& w : dead) {
+      if (w->pid > 0) kill(-w->pid, SIGKILL);
+      if (w->state == WorkerState::Spawning || w->state == WorkerState::Connected) {
+        if (w->pooled) spawning_[w->kind]--;
+        if (w->kind == kDirect) inflight_spawns_--;
+      }
+      auto& q = ready_[w->kind];
+      for (auto r = q.begin(); r != q.end(); ++r)
+        if (*r == w) {
+          q.erase(r);
+          break;
+        }
+      w->exited = true;
+      w->exit_code = -1;
+      w->state = WorkerState::Exited;
+      workers_.erase(w->id);
+      if (w->pid > 0) by_pid_.erase(w->pid);
+      cleanup_dirs_.push_back(w->dir);
     }
-    inflight_spawns_ = 0;
-    spawn_queue_.clear();
   }
   cv_.notify_all();
   sleep(1);
   std::string err;
   {
-    std::lock_guard<std::mutex> lk(zygote_write_mu_);
-    close(zygote_fd_);
-    zygote_fd_ = -1;
+    std::lock_guard<std::mutex> lk(z->write_mu);
+    close(z->fd);
+    z->fd = -1;
   }
-  if (!start_zygote(&err)) {
-    BEE_ERROR("zygote restart failed: %s", err.c_str());
+  if (!start_zygote(z, &err)) {
+    BEE_ERROR("zygote %d restart failed: %s", z->index, err.c_str());
     return;
   }
   std::lock_guard<std::mutex> lk(mu_);
@@ -366,12 +419,16 @@ std::shared_ptr<Worker> SandboxPool::spawn_worker(bool pooled, int kind, const s
   msg.set("id", w->id);
   msg.set("cwd", w->ws);
   msg.set("env", env);
+  Zygote* z = pick_zygote(kind);
+  w->zygote = z->index;
   workers_[w->id] = w;
   if (pooled) spawning_[kind]++;
   m_spawned_++;
-  if (inflight_spawns_ < cfg_.max_concurrent_spawns || !pooled) {
-    inflight_spawns_++;
-    send_zygote(msg);
+  // only direct warm-ups (hipInit) contend in the driver: cap those in flight;
+  // light sandboxes never touch HIP and are forked as fast as asked
+  if (kind == kLight || !pooled || inflight_spawns_ < cfg_.max_concurrent_spawns) {
+    if (kind == kDirect) inflight_spawns_++;
+    send_zygote(z, msg);
   } else {
     spawn_queue_.emplace_back(w, msg);
   }
@@ -379,14 +436,14 @@ std::shared_ptr<Worker> SandboxPool::spawn_worker(bool pooled, int kind, const s
 }
 
 void SandboxPool::refill_locked() {
-  if (stopping_ || !zygote_alive_) return;
-  // release queued spawns as slots free up
+  if (stopping_ || !any_zygote_alive()) return;
+  // release queued (direct) spawns as slots free up
   while (!spawn_queue_.empty() && inflight_spawns_ < cfg_.max_concurrent_spawns) {
     auto item = spawn_queue_.front();
     spawn_queue_.pop_front();
     if (item.first->state != WorkerState::Spawning) continue;
     inflight_spawns_++;
-    send_zygote(item.second);
+    send_zygote(zygotes_[item.first->zygote].get(), item.second);
   }
   for (int k = 0; k < 2; ++k) {
     while ((int)ready_[k].size() + spawning_[k] < target_of(k)) spawn_worker(true, k, cfg_.gpus, Json::object());
@@ -454,8 +511,9 @@ void SandboxPool::worker_reader(int fd) {
         w->t_ready = mono_ms();
         w->warm_ms = m["warm_ms"].as_number();
         m_warm_ms_sum_ += w->t_ready - w->t_spawn;
+        m_worker_warm_ms_sum_ += w->warm_ms;
         m_warm_count_++;
-        inflight_spawns_--;
+        if (w->kind == kDirect) inflight_spawns_--;
         if (w->pooled) {
           spawning_[w->kind]--;
           ready_[w->kind].push_back(w);
@@ -464,6 +522,10 @@ void SandboxPool::worker_reader(int fd) {
           BEE_WARN("worker %s: GPU warm-up failed: %s", w->id.c_str(), m["gpu_error"].as_string().c_str());
         refill_locked();
       }
+    } else if (op == "done" && w) {
+      w->done = true;
+      w->done_code = (int)m["code"].as_int();
+      w->t_exit = mono_ms();
     }
     lk.unlock();
     cv_.notify_all();
@@ -522,7 +584,7 @@ void SandboxPool::destroy(const std::shared_ptr<Worker>& w) {
   }
   if (w->state == WorkerState::Spawning || w->state == WorkerState::Connected) {
     // destroyed before it reported ready: release its spawn slot exactly once
-    inflight_spawns_--;
+    if (w->kind == kDirect) inflight_spawns_--;
     if (w->pooled) spawning_[w->kind]--;
     w->state = WorkerState::Failed;
   }
@@ -716,6 +778,7 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   }
   bool died = false;
   for (auto& w : ranks) {
+    w->t_run = mono_ms();
     RunResult rr = run_in(w, spec);
     if (rr.died) died = true;
   }
@@ -723,9 +786,9 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   {
     std::unique_lock<std::mutex> lk(mu_);
     auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds((int64_t)(timeout_s * 1000));
-    auto all_exited = [&] {
+    auto all_exited = [&] {  // finished = reported done (outputs flushed) or exited
       for (auto& w : ranks)
-        if (!w->exited) return false;
+        if (!w->exited && !w->done) return false;
       return true;
     };
     while (!all_exited() && !died) {
@@ -757,7 +820,7 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
     bool trunc = false;
     out_all += read_file_capped(join_path(ranks[r]->meta, "stdout"), cfg_.max_output_bytes - (int64_t)out_all.size(), &trunc);
     err_all += read_file_capped(join_path(ranks[r]->meta, "stderr"), cfg_.max_output_bytes - (int64_t)err_all.size(), &trunc);
-    if (exit_code == 0 && ranks[r]->exit_code != 0) exit_code = ranks[r]->exit_code;
+    if (exit_code == 0 && ranks[r]->final_code() != 0) exit_code = ranks[r]->final_code();
   }
   if (died && exit_code == 0) exit_code = -1;
   if (timed_out) {
@@ -796,6 +859,8 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
     }
   }
   tm.collect_ms = mono_ms() - t3;
+  bool tj_trunc = false;
+  const std::string timing_text = read_file_capped(join_path(lead->meta, "timing.json"), 4096, &tj_trunc);
   cleanup_all();
   tm.total_ms = mono_ms() - t0;
   {
@@ -807,7 +872,24 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   resp.set("stderr", err_all);
   resp.set("exit_code", exit_code);
   resp.set("files", files);
-  resp.set("timings_ms", timings_json(tm));
+  Json timings = timings_json(tm);
+  {
+    // worker-side phase stamps (same CLOCK_MONOTONIC): where "run" went
+    try {
+      Json st = timing_text.empty() ? Json::object() : Json::parse(timing_text);
+      const double recv = st["recv"].as_number(), s0 = st["script_start"].as_number(),
+                   s1 = st["script_end"].as_number(), ex = st["exit"].as_number();
+      if (recv > 0 && s0 > 0 && s1 > 0 && ex > 0) {
+        timings.set("w_dispatch", recv - lead->t_run);
+        timings.set("w_setup", s0 - recv);
+        timings.set("w_script", s1 - s0);
+        timings.set("w_atexit", ex - s1);
+        timings.set("w_reap", lead->t_exit - ex);
+      }
+    } catch (...) {
+    }
+  }
+  resp.set("timings_ms", timings);
   resp.set("worker", lead->id);
   resp.set("gpus", lead->gpus);
   resp.set("warm_ms", lead->warm_ms);
@@ -842,10 +924,17 @@ Json SandboxPool::status() {
   j.set("queued_spawns", (int64_t)spawn_queue_.size());
   j.set("workers", (int64_t)workers_.size());
   j.set("inflight", (int64_t)m_inflight_.load());
-  j.set("zygote_alive", zygote_alive_.load());
+  j.set("zygote_alive", healthy());
+  int64_t zalive = 0;
+  for (auto& z : zygotes_) zalive += z->alive ? 1 : 0;
+  j.set("zygotes", (int64_t)zygotes_.size());
+  j.set("zygotes_alive", zalive);
   j.set("pod_mode", cfg_.pod_mode);
   j.set("executions", (int64_t)m_exec_total_.load());
   j.set("mean_warm_ms", m_warm_count_ ? m_warm_ms_sum_ / (double)m_warm_count_ : 0.0);
+  j.set("mean_worker_warm_ms", m_warm_count_ ? m_worker_warm_ms_sum_ / (double)m_warm_count_ : 0.0);
+  j.set("mean_fork_ms", m_fork_count_ ? m_fork_ms_sum_ / (double)m_fork_count_ : 0.0);
+  j.set("mean_acquire_ms", m_exec_total_ ? m_acquire_ms_sum_ / (double)m_exec_total_.load() : 0.0);
   Json states = Json::object();
   std::map<std::string, int64_t> counts;
   for (auto& kv : workers_) counts[state_name(kv.second->state)]++;

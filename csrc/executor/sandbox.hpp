@@ -50,6 +50,8 @@ struct PoolConfig {
   // beekern through it and never initialise HIP themselves
   std::string broker_lib;              // path of libbeekern.so ("" = no broker)
   int light_target = 8;                // warm light sandboxes kept ready
+  int light_zygotes = 2;               // parallel forkers for light sandboxes
+  std::string light_preload = "numpy,pandas,scipy.stats,matplotlib.pyplot,PIL.Image,bee_code_interpreter_fs_amd.ops";
 };
 
 enum WorkerKind { kDirect = 0, kLight = 1 };
@@ -63,18 +65,35 @@ struct Worker {
   pid_t pid = -1;
   int fd = -1;
   WorkerState state = WorkerState::Spawning;
-  double t_spawn = 0, t_ready = 0;
+  double t_spawn = 0, t_ready = 0, t_run = 0, t_exit = 0;  // CLOCK_MONOTONIC ms
   double warm_ms = 0;
   bool exited = false;
   int exit_code = 0;
+  bool done = false;  // worker reported completion (outputs flushed) before exiting
+  int done_code = 0;
+  int final_code() const { return done ? done_code : exit_code; }
   int term_signal = 0;
   bool pooled = true;  // false: dedicated (gang / custom env) worker
   int kind = kDirect;
+  int zygote = 0;  // index of the zygote that forked it
   int64_t hbm_quota = 0;
   std::string fail_reason;
 };
 
 class KernelBroker;
+
+// A pre-imported Python process that forks sandboxes.  Zygote 0 preloads
+// torch (direct sandboxes); light zygotes preload only the CPU stack, fork
+// ~2x faster and run in parallel so refills keep up with the request rate.
+struct Zygote {
+  int index = 0;
+  int kind = kDirect;
+  pid_t pid = -1;
+  int fd = -1;
+  std::thread thread;
+  std::mutex write_mu;
+  std::atomic<bool> alive{false};
+};
 
 struct ExecTimings {
   double acquire_ms = 0, stage_ms = 0, run_ms = 0, collect_ms = 0, total_ms = 0;
@@ -95,13 +114,15 @@ class SandboxPool {
   Json status();
   std::string metrics_text();
   const PoolConfig& config() const { return cfg_; }
-  bool healthy() const { return zygote_alive_.load(); }
+  bool healthy() const { return !zygotes_.empty() && zygotes_[0]->alive.load(); }
 
  private:
   // zygote
-  bool start_zygote(std::string* err);
-  void zygote_reader();
-  void send_zygote(const Json& msg);
+  bool start_zygote(Zygote* z, std::string* err);
+  void zygote_reader(Zygote* z);
+  void send_zygote(Zygote* z, const Json& msg);
+  Zygote* pick_zygote(int kind);
+  bool any_zygote_alive() const;
   // workers
   void worker_acceptor();
   void worker_reader(int fd);
@@ -142,14 +163,12 @@ class SandboxPool {
   int inflight_spawns_ = 0;
   std::deque<std::pair<std::shared_ptr<Worker>, Json>> spawn_queue_;
 
-  pid_t zygote_pid_ = -1;
-  int zygote_fd_ = -1;
-  std::mutex zygote_write_mu_;
-  std::atomic<bool> zygote_alive_{false};
+  std::vector<std::unique_ptr<Zygote>> zygotes_;  // [0] = direct (torch), rest light
+  std::atomic<uint64_t> rr_{0};
   std::atomic<bool> stopping_{false};
   int worker_listen_fd_ = -1;
   std::string worker_sock_path_;
-  std::thread zygote_thread_, acceptor_thread_, cleanup_thread_;
+  std::thread acceptor_thread_, cleanup_thread_;
   std::mutex cleanup_mu_;
   std::condition_variable cleanup_cv_;
   std::deque<std::string> cleanup_dirs_;
@@ -158,8 +177,8 @@ class SandboxPool {
   // metrics
   std::atomic<int64_t> m_exec_total_{0}, m_exec_failed_{0}, m_timeouts_{0}, m_spawned_{0}, m_spawn_failed_{0};
   std::atomic<int64_t> m_inflight_{0};
-  double m_warm_ms_sum_ = 0, m_exec_ms_sum_ = 0, m_acquire_ms_sum_ = 0;
-  int64_t m_warm_count_ = 0;
+  double m_warm_ms_sum_ = 0, m_exec_ms_sum_ = 0, m_acquire_ms_sum_ = 0, m_fork_ms_sum_ = 0, m_worker_warm_ms_sum_ = 0;
+  int64_t m_warm_count_ = 0, m_fork_count_ = 0;
 };
 
 }  // namespace bee
