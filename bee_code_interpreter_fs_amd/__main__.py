@@ -1,18 +1,32 @@
-"""``python -m bee_code_interpreter_fs_amd``: gRPC + HTTP servers in one loop.
+"""``python -m bee_code_interpreter_fs_amd``: gRPC + HTTP servers.
 
 Parity with `src/code_interpreter/__main__.py:22-36` (uvicorn + grpc.aio under
-one event loop, graceful shutdown); the executor backend (GPU-pinned
-sandbox pools) is started before either server accepts requests.
+one event loop, graceful shutdown); the executor backend (GPU-pinned sandbox
+pools) is started before either server accepts requests.
+
+Scale-out (``APP_FRONTEND_PROCESSES`` > 1, local backend): this process
+becomes a supervisor that owns the per-GPU native executors and starts N
+front-end replicas.  Replicas bind the same gRPC/HTTP ports with
+SO_REUSEPORT (the kernel spreads connections), attach to the shared
+executors, and coordinate gangs through the daemons' reservation API — a
+single Python front-end tops out at a few thousand RPC/s, 8 MI355X pools
+serve more.
 """
 
 from __future__ import annotations
 
 import asyncio
+import json
+import os
 import signal
+import socket
+import subprocess
+import sys
 
 import uvicorn
 
 from .application_context import ApplicationContext
+from .config import Config
 
 
 def _split_addr(addr: str):
@@ -20,24 +34,117 @@ def _split_addr(addr: str):
     return host or "0.0.0.0", int(port)
 
 
-async def main() -> None:
-    ctx = ApplicationContext()
-    await ctx.start()
+def _reuseport_socket(host: str, port: int) -> socket.socket:
+    family = socket.AF_INET6 if ":" in host else socket.AF_INET
+    s = socket.socket(family, socket.SOCK_STREAM)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+    s.bind((host, port))
+    s.listen(2048)
+    s.setblocking(False)
+    return s
+
+
+def _free_port(host: str) -> int:
+    with socket.socket() as s:
+        s.bind((host, 0))
+        return s.getsockname()[1]
+
+
+async def _serve(ctx: ApplicationContext, stop: asyncio.Event) -> None:
     host, port = _split_addr(ctx.config.http_listen_addr)
     http = uvicorn.Server(uvicorn.Config(ctx.http_server, host=host, port=port, loop="asyncio", log_level="warning"))
-    http.install_signal_handlers = lambda: None  # handled below
-    stop = asyncio.Event()
-    loop = asyncio.get_running_loop()
-    for sig in (signal.SIGINT, signal.SIGTERM):
-        loop.add_signal_handler(sig, stop.set)
+    http.install_signal_handlers = lambda: None  # handled by the caller
+    sock = _reuseport_socket(host, port)
     await ctx.grpc_server.start(ctx.config.grpc_listen_addr)
-    http_task = asyncio.create_task(http.serve())
+    http_task = asyncio.create_task(http.serve(sockets=[sock]))
+    print(f"BEE_SERVICE_READY grpc={ctx.config.grpc_listen_addr} http={ctx.config.http_listen_addr}", flush=True)
     try:
         await stop.wait()
     finally:
         http.should_exit = True
         await ctx.grpc_server.stop(grace=5)
         await http_task
+
+
+def _install_stop(loop) -> asyncio.Event:
+    stop = asyncio.Event()
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        loop.add_signal_handler(sig, stop.set)
+    return stop
+
+
+async def main() -> None:
+    config = Config()
+    n_frontends = config.frontend_processes
+    if config.executor_backend == "local" and n_frontends != 1 and not os.environ.get("BEE_FRONTEND_ATTACH"):
+        await supervise(config, n_frontends)
+        return
+    ctx = ApplicationContext(config)
+    stop = _install_stop(asyncio.get_running_loop())
+    await ctx.start()
+    try:
+        await _serve(ctx, stop)
+    finally:
+        await ctx.close()
+
+
+async def supervise(config: Config, n_frontends: int) -> None:
+    """Own the executors; run front-end replicas as child processes."""
+    ctx = ApplicationContext(config)
+    backend = ctx.code_executor
+    await backend.start()
+    if n_frontends <= 0:
+        n_frontends = max(1, min(8, len(backend.slots)))
+    ghost, gport = _split_addr(config.grpc_listen_addr)
+    hhost, hport = _split_addr(config.http_listen_addr)
+    gport = gport or _free_port(ghost)
+    hport = hport or _free_port(hhost)
+    env = dict(os.environ)
+    env.update(
+        {
+            "BEE_FRONTEND_ATTACH": backend.attach_spec(),
+            "APP_GRPC_LISTEN_ADDR": f"{ghost}:{gport}",
+            "APP_HTTP_LISTEN_ADDR": f"{hhost}:{hport}",
+            "APP_FRONTEND_PROCESSES": "1",
+        }
+    )
+    children = []
+    for i in range(n_frontends):
+        e = dict(env, BEE_FRONTEND_INDEX=str(i))
+        children.append(subprocess.Popen([sys.executable, "-m", "bee_code_interpreter_fs_amd"], env=e, stdout=subprocess.PIPE))
+    loop = asyncio.get_running_loop()
+    for c in children:  # wait until every replica serves
+        line = await loop.run_in_executor(None, c.stdout.readline)
+        if not line.startswith(b"BEE_SERVICE_READY"):
+            raise RuntimeError(f"front-end replica failed to start: {line!r}")
+    print(
+        f"BEE_SERVICE_READY grpc={ghost}:{gport} http={hhost}:{hport} frontends={n_frontends} "
+        f"slots={json.loads(backend.attach_spec())!r}",
+        flush=True,
+    )
+    stop = _install_stop(loop)
+    try:
+        while not stop.is_set():
+            try:
+                await asyncio.wait_for(stop.wait(), 2.0)
+            except asyncio.TimeoutError:
+                pass
+            for i, c in enumerate(children):
+                if c.poll() is not None and not stop.is_set():  # replica died: replace it
+                    e = dict(env, BEE_FRONTEND_INDEX=str(i))
+                    children[i] = subprocess.Popen(
+                        [sys.executable, "-m", "bee_code_interpreter_fs_amd"], env=e, stdout=subprocess.DEVNULL
+                    )
+    finally:
+        for c in children:
+            if c.poll() is None:
+                c.send_signal(signal.SIGTERM)
+        for c in children:
+            try:
+                c.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                c.kill()
         await ctx.close()
 
 

@@ -92,6 +92,9 @@ class Config:
     broker_enabled: bool = True
     # zygote processes forking light sandboxes per GPU (fork parallelism)
     light_zygotes_per_gpu: int = 2
+    # front-end (gRPC + HTTP) replica processes sharing the ports via
+    # SO_REUSEPORT and the node's executors (0 = one per GPU, max 8)
+    frontend_processes: int = 1
     # concurrent executions admitted per GPU pool (others queue)
     max_inflight_per_gpu: int = 16
     # per-sandbox HBM quota in bytes (0 = 288 GB / max_inflight_per_gpu minus reserve)

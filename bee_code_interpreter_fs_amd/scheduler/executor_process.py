@@ -2,7 +2,7 @@
 
 The daemon binds a Unix socket (local backend) and prints
 ``BEE_EXECUTOR_LISTENING <addr>`` once it accepts connections; requests are
-HTTP/1.1 JSON over that socket (httpx UDS transport, keep-alive).
+HTTP/1.1 JSON over that socket (keep-alive pool, ``uds_http``).
 """
 
 from __future__ import annotations
@@ -16,7 +16,7 @@ import subprocess
 import sys
 from typing import List, Optional
 
-import httpx
+from .uds_http import Response, UdsHttpClient
 
 logger = logging.getLogger("executor_client")
 
@@ -71,7 +71,7 @@ class ExecutorProcess:
         self.use_interposer = use_interposer
         self.proc: Optional[subprocess.Popen] = None
         self.address: Optional[str] = None
-        self.client: Optional[httpx.AsyncClient] = None
+        self.client: Optional[UdsHttpClient] = None
         self._log_task: Optional[asyncio.Task] = None
 
     def command(self, socket_path: str) -> List[str]:
@@ -133,25 +133,30 @@ class ExecutorProcess:
             self.stop()
             raise RuntimeError(f"executor {self.name} failed to start: {text!r}")
         self.address = text.split(" ", 1)[1]
-        path = self.address[len("unix:") :]
-        transport = httpx.AsyncHTTPTransport(uds=path)
-        self.client = httpx.AsyncClient(
-            transport=transport, base_url="http://executor", timeout=httpx.Timeout(None, connect=10.0)
-        )
+        self.client = UdsHttpClient(self.address[len("unix:") :])
         logger.info("executor %s up at %s (gpus=%r, target=%d)", self.name, self.address, self.gpus, self.target)
 
-    def alive(self) -> bool:
-        return self.proc is not None and self.proc.poll() is None
+    def attach(self, address: str) -> None:
+        """Use a daemon started by another process (multi-process front-end)."""
+        self.address = address
+        self.client = UdsHttpClient(address[len("unix:") :])
 
-    async def post(self, path: str, body: dict, timeout: Optional[float] = None) -> httpx.Response:
+    @property
+    def socket_path(self) -> Optional[str]:
+        return self.address[len("unix:") :] if self.address else None
+
+    def alive(self) -> bool:
+        if self.proc is not None:
+            return self.proc.poll() is None
+        return self.address is not None and os.path.exists(self.socket_path)
+
+    async def post(self, path: str, body: dict, timeout: Optional[float] = None) -> Response:
         assert self.client is not None
-        return await self.client.post(path, json=body, timeout=timeout)
+        return await self.client.post_json(path, body, timeout)
 
     async def get_json(self, path: str) -> dict:
         assert self.client is not None
-        r = await self.client.get(path, timeout=10.0)
-        r.raise_for_status()
-        return r.json()
+        return await self.client.get_json(path)
 
     async def wait_ready(self, min_ready: int = 1, timeout: float = 300.0) -> dict:
         """Wait until the pool has ``min_ready`` warm sandboxes."""

@@ -25,20 +25,23 @@ Replaces the reference's Kubernetes pod pool (`kubernetes_code_executor.py:
 from __future__ import annotations
 
 import asyncio
+import json
 import logging
 import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
-import httpx
-
 from ..config import Config
 from ..services.storage import Storage
 from .backend import CodeExecutor, ExecuteRequest, ExecutionResult
 from .executor_process import ExecutorProcess
+from .uds_http import UdsHttpError
 
 logger = logging.getLogger("local_gpu_pool")
+
+# JSON list of {index, gpu, address}: set for front-end replica processes
+ATTACH_ENV = "BEE_FRONTEND_ATTACH"
 
 
 def detect_gpus() -> List[int]:
@@ -85,6 +88,8 @@ class LocalGpuPoolBackend(CodeExecutor):
         self.gpu_ids: List[int] = list(ids or [])
         self.default_gpus = 1 if self.gpu_ids else 0
         self.slots: List[Slot] = []
+        self.attached = False
+        self._rr = int(os.environ.get("BEE_FRONTEND_INDEX", "0"))
         self._cond: Optional[asyncio.Condition] = None
         self._tasks: set = set()
         self.stats_ = PoolStats()
@@ -95,12 +100,27 @@ class LocalGpuPoolBackend(CodeExecutor):
     # ---- lifecycle --------------------------------------------------------------------
     async def start(self) -> None:
         self._cond = asyncio.Condition()
+        attach = os.environ.get(ATTACH_ENV)
+        if attach:
+            # front-end replica: the executors belong to the supervisor process
+            for entry in json.loads(attach):
+                ex = self._make_executor(entry["index"], entry["gpu"])
+                ex.attach(entry["address"])
+                self.slots.append(Slot(index=entry["index"], gpu=entry["gpu"], executor=ex))
+            self.gpu_ids = [s.gpu for s in self.slots if s.gpu is not None]
+            self.default_gpus = 1 if self.gpu_ids else 0
+            self.attached = True
+            return
         devices: List[Optional[int]] = list(self.gpu_ids) or [None]
         for i, gpu in enumerate(devices):
             ex = self._make_executor(i, gpu)
             self.slots.append(Slot(index=i, gpu=gpu, executor=ex))
         await asyncio.gather(*(s.executor.start() for s in self.slots))
         logger.info("local pool: %d slot(s) on GPUs %s", len(self.slots), self.gpu_ids or "[cpu]")
+
+    def attach_spec(self) -> str:
+        """What front-end replicas need to share this pool's executors."""
+        return json.dumps([{"index": s.index, "gpu": s.gpu, "address": s.executor.address} for s in self.slots])
 
     def _make_executor(self, i: int, gpu: Optional[int]) -> ExecutorProcess:
         c = self.config
@@ -148,7 +168,10 @@ class LocalGpuPoolBackend(CodeExecutor):
             while True:
                 cands = [s for s in self.slots if self._admissible(s, hbm)]
                 if cands:
-                    slot = min(cands, key=lambda s: (s.inflight, s.hbm_committed, s.index))
+                    # least loaded; ties rotate so replicas and bursts spread over GPUs
+                    self._rr += 1
+                    n = len(self.slots)
+                    slot = min(cands, key=lambda s: (s.inflight, s.hbm_committed, (s.index - self._rr) % n))
                     slot.inflight += 1
                     slot.hbm_committed += hbm
                     return slot
@@ -213,8 +236,15 @@ class LocalGpuPoolBackend(CodeExecutor):
         if want == 0 or not self.gpu_ids:
             hbm = 0
         slots = await self._acquire_gang(want, hbm) if gang else [await self._acquire_one(hbm)]
-        t_acq = time.perf_counter()
         lead = slots[0]
+        gang_lock = None
+        if gang:
+            try:
+                gang_lock = await self._reserve_gpus(slots, float(request.timeout or self.config.default_timeout))
+            except BaseException:
+                await self._release(slots, hbm, gang)
+                raise
+        t_acq = time.perf_counter()
         try:
             body = {
                 "files": {p: self.storage.path_of(h) for p, h in request.files.items()},
@@ -234,13 +264,14 @@ class LocalGpuPoolBackend(CodeExecutor):
             if gang:
                 body["gpus"] = ",".join(str(s.gpu) for s in slots)
                 body["nprocs"] = int(request.nprocs)
+                body["gang"] = True
             elif want == 0 and lead.gpu is not None:
                 body["gpus"] = ""  # CPU-only sandbox on a GPU slot
             if request.env:
                 body["env"] = dict(request.env)
             try:
                 resp = await lead.executor.post("/v1/execute", body, timeout=body["timeout"] + 180.0)
-            except (httpx.TransportError, AssertionError) as e:
+            except (UdsHttpError, OSError, AssertionError) as e:
                 self._mark_failed(lead, str(e))
                 raise _SlotFailure(f"slot {lead.index}: {e}") from e
             if resp.status_code == 503:
@@ -250,6 +281,8 @@ class LocalGpuPoolBackend(CodeExecutor):
                 raise ValueError(detail) if resp.status_code in (400, 422) else RuntimeError(detail)
             data = resp.json()
         finally:
+            if gang:
+                await self._unreserve_gpus(slots, gang_lock)
             await self._release(slots, hbm, gang)
         t1 = time.perf_counter()
         timings = dict(data.get("timings_ms") or {})
@@ -268,6 +301,39 @@ class LocalGpuPoolBackend(CodeExecutor):
             timings_ms=timings,
             gpu_ids=[s.gpu for s in slots if s.gpu is not None] if want else [],
         )
+
+    # ---- cross-process gang reservation ---------------------------------------------
+    def _gang_lock_path(self) -> str:
+        os.makedirs(self.config.sandbox_root, exist_ok=True)
+        return os.path.join(self.config.sandbox_root, "gang.lock")
+
+    async def _reserve_gpus(self, slots: List[Slot], timeout: float) -> int:
+        """Front-end replicas share executors, so a gang also reserves its
+        GPUs in the daemons: a node-wide flock serialises gangs (no two can
+        deadlock holding half each other's GPUs), each daemon stops admitting
+        new jobs and drains, the reservation expiring on its own if this
+        process dies."""
+        import fcntl
+
+        loop = asyncio.get_running_loop()
+        fd = os.open(self._gang_lock_path(), os.O_RDWR | os.O_CREAT, 0o600)
+        try:
+            await loop.run_in_executor(None, fcntl.flock, fd, fcntl.LOCK_EX)
+            ttl = timeout + 120.0
+            resps = await asyncio.gather(
+                *(s.executor.post("/v1/reserve", {"ttl": ttl, "wait": ttl}, timeout=ttl + 30) for s in slots)
+            )
+            if any(r.status_code != 200 for r in resps):
+                raise RuntimeError("could not drain the gang's GPUs: " + ", ".join(r.text for r in resps))
+        except BaseException:
+            await self._unreserve_gpus(slots, fd)
+            raise
+        return fd
+
+    async def _unreserve_gpus(self, slots: List[Slot], fd: Optional[int]) -> None:
+        await asyncio.gather(*(s.executor.post("/v1/release", {}, timeout=30) for s in slots), return_exceptions=True)
+        if fd is not None:
+            os.close(fd)  # drops the flock
 
     def _mark_failed(self, slot: Slot, error: str) -> None:
         slot.failures += 1
@@ -346,7 +412,7 @@ def sandbox_mode(request: ExecuteRequest, storage: Storage) -> str:
     return "direct" if DIRECT_GPU_MODULES.intersection(imported_modules(source or "")) else "light"
 
 
-def _detail(resp: httpx.Response) -> str:
+def _detail(resp) -> str:
     try:
         return str(resp.json().get("detail", resp.text))
     except Exception:

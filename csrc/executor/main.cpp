@@ -161,6 +161,27 @@ int main(int argc, char** argv) {
       resp.json(200, pool.status().dump());
       return;
     }
+    if (req.method == "POST" && (p == "/v1/reserve" || p == "/v1/release")) {
+      Json body;
+      try {
+        std::string text = req.body->read_all(1 << 16);
+        body = text.empty() ? Json::object() : Json::parse(text);
+      } catch (const std::exception& e) {
+        resp.error(422, e.what());
+        return;
+      }
+      Json j = Json::object();
+      if (p == "/v1/reserve") {
+        const bool drained = pool.reserve(body["ttl"].as_number(600), body["wait"].as_number(600));
+        j.set("drained", drained);
+        resp.json(drained ? 200 : 409, j.dump());
+      } else {
+        pool.release();
+        j.set("released", true);
+        resp.json(200, j.dump());
+      }
+      return;
+    }
     if (req.method == "GET" && p == "/metrics") {
       resp.status = 200;
       resp.content_type = "text/plain; version=0.0.4";

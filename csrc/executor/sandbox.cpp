@@ -670,6 +670,24 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
     std::atomic<int64_t>& c;
     ~InflightGuard() { c--; }
   } guard{m_inflight_};
+  {
+    // a gang reservation holds new jobs back (the gang's own job bypasses it)
+    std::unique_lock<std::mutex> lk(mu_);
+    const bool bypass = req["gang"].as_bool(false);
+    while (!bypass && reserved_ && mono_ms() < reserved_until_ && !stopping_)
+      cv_.wait_for(lk, std::chrono::milliseconds(50));
+    jobs_++;
+  }
+  struct JobGuard {
+    SandboxPool* p;
+    ~JobGuard() {
+      {
+        std::lock_guard<std::mutex> lk(p->mu_);
+        p->jobs_--;
+      }
+      p->cv_.notify_all();
+    }
+  } job_guard{this};
 
   const double timeout_s = req["timeout"].is_number() && req["timeout"].as_number() > 0 ? req["timeout"].as_number()
                                                                                          : cfg_.default_timeout_s;
@@ -897,6 +915,23 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
 }
 
 Json SandboxPool::execute(const Json& req, int* http_status) { return run_job(req, http_status, false); }
+
+bool SandboxPool::reserve(double ttl_s, double wait_s) {
+  std::unique_lock<std::mutex> lk(mu_);
+  reserved_ = true;
+  reserved_until_ = mono_ms() + ttl_s * 1e3;
+  const double deadline = mono_ms() + wait_s * 1e3;
+  while (jobs_ > 0 && mono_ms() < deadline && !stopping_) cv_.wait_for(lk, std::chrono::milliseconds(20));
+  return jobs_ == 0;
+}
+
+void SandboxPool::release() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    reserved_ = false;
+  }
+  cv_.notify_all();
+}
 
 Json SandboxPool::execute_pod(const Json& req, int* http_status) {
   std::lock_guard<std::mutex> lk(pod_mu_);

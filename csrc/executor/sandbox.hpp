@@ -113,6 +113,10 @@ class SandboxPool {
 
   Json status();
   std::string metrics_text();
+  // gang support across front-end processes: stop admitting new jobs on this
+  // GPU, wait until running ones drain; expires after ttl_s
+  bool reserve(double ttl_s, double wait_s);
+  void release();
   const PoolConfig& config() const { return cfg_; }
   bool healthy() const { return !zygotes_.empty() && zygotes_[0]->alive.load(); }
 
@@ -160,6 +164,9 @@ class SandboxPool {
   std::deque<std::shared_ptr<Worker>> ready_[2];  // by WorkerKind
   int spawning_[2] = {0, 0};
   std::unique_ptr<KernelBroker> broker_;
+  int64_t jobs_ = 0;            // admitted jobs (guarded by mu_)
+  bool reserved_ = false;       // a gang holds this GPU
+  double reserved_until_ = 0;   // mono ms
   int inflight_spawns_ = 0;
   std::deque<std::pair<std::shared_ptr<Worker>, Json>> spawn_queue_;
 
