@@ -91,7 +91,7 @@ class Config:
     # run the per-GPU kernel broker in the executor daemon
     broker_enabled: bool = True
     # zygote processes forking light sandboxes per GPU (fork parallelism)
-    light_zygotes_per_gpu: int = 2
+    light_zygotes_per_gpu: int = 4
     # front-end (gRPC + HTTP) replica processes sharing the ports via
     # SO_REUSEPORT and the node's executors (0 = one per GPU, max 8)
     frontend_processes: int = 1

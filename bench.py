@@ -67,6 +67,12 @@ def percentile(xs, q):
     return xs[k]
 
 
+def visible_gpus() -> int:
+    import torch
+
+    return max(torch.cuda.device_count(), 1)
+
+
 def free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -81,7 +87,9 @@ def start_service(tmp: str, n_gpus: int, args):
         {
             "APP_GRPC_LISTEN_ADDR": f"127.0.0.1:{gport}",
             "APP_HTTP_LISTEN_ADDR": f"127.0.0.1:{hport}",
-            "APP_GPU_IDS": json.dumps(list(range(n_gpus))),
+            # one executor per physical GPU (a rehearsal with more ranks than
+            # GPUs folds the extra ranks onto the existing devices)
+            "APP_GPU_IDS": json.dumps(sorted({i % visible_gpus() for i in range(n_gpus)})),
             "APP_FILE_STORAGE_PATH": os.path.join(tmp, "files"),
             "APP_SANDBOX_ROOT": os.path.join(tmp, "sandboxes"),
             "APP_WORKERS_PER_GPU_TARGET": "1",  # direct sandboxes: the payload does not need them
@@ -202,7 +210,7 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local % visible_gpus())
 
     def barrier():
         if world > 1:
