@@ -14,6 +14,7 @@ import shutil
 import signal
 import subprocess
 import sys
+import tempfile
 from typing import List, Optional
 
 from .uds_http import Response, UdsHttpClient
@@ -107,6 +108,8 @@ class ExecutorProcess:
         run_dir = os.path.join(self.sandbox_root, ".run")
         os.makedirs(run_dir, exist_ok=True)
         sock = os.path.join(run_dir, "executor.sock")
+        if len(sock) > 100:  # AF_UNIX path limit (108 bytes)
+            sock = os.path.join(tempfile.mkdtemp(prefix="bee-"), "executor.sock")
         env = dict(os.environ)
         env.update(self.extra_env)
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")

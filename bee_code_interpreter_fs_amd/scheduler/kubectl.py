@@ -34,7 +34,9 @@ Input = Union[bytes, str, list, dict, None]
 
 
 def _flags(kwargs: Dict[str, Any]) -> Dict[str, Any]:
-    return {k.lstrip("_").replace("_", "-"): v for k, v in kwargs.items() if v}
+    # None/False/"" drop the flag; 0 is a real value (--grace-period=0), which
+    # the reference's truthiness filter silently dropped
+    return {k.lstrip("_").replace("_", "-"): v for k, v in kwargs.items() if v is not None and v is not False and v != ""}
 
 
 class Kubectl:

@@ -189,7 +189,8 @@ class KubernetesBackend(CodeExecutor):
         t0 = time.perf_counter()
         timeout = float(request.timeout or self.default_timeout)
         async with self.executor_pod() as pod, httpx.AsyncClient(timeout=timeout + 30) as client:
-            base = f"http://{pod['status']['podIP']}:{EXECUTOR_PORT}"
+            port = int(pod["metadata"].get("annotations", {}).get("bee.executor/port", EXECUTOR_PORT))
+            base = f"http://{pod['status']['podIP']}:{port}"
 
             async def upload(path: str, obj: str):
                 root, rel = split_logical_path(path)

@@ -68,6 +68,9 @@ const char* state_name(WorkerState s) {
 
 SandboxPool::SandboxPool(PoolConfig cfg) : cfg_(std::move(cfg)) {
   if (cfg_.run_dir.empty()) cfg_.run_dir = join_path(cfg_.sandbox_root, ".run");
+  // Unix socket paths are capped at 107 bytes: deep sandbox roots get their
+  // control sockets in a short private directory instead
+  if (cfg_.run_dir.size() > 72) cfg_.run_dir = "/tmp/bee-run-" + random_hex(6);
 }
 
 SandboxPool::~SandboxPool() { stop(); }

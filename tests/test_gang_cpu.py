@@ -1,0 +1,85 @@
+"""Gang sandboxes on CPU: nprocs=2 ranks launched by the native executor with
+torch.distributed rendezvous env, all-reducing over gloo (the same path an
+8-GPU RCCL job takes, minus the GPUs)."""
+
+import asyncio
+import os
+import tempfile
+
+import pytest
+
+from bee_code_interpreter_fs_amd.config import Config
+from bee_code_interpreter_fs_amd.parallel import rank_env
+from bee_code_interpreter_fs_amd.scheduler.executor_process import ExecutorProcess
+
+from .harness import ensure_native_executor
+
+GANG = """
+import os, torch, torch.distributed as dist
+dist.init_process_group("gloo", rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]))
+x = torch.tensor([float(dist.get_rank() + 1)])
+dist.all_reduce(x)
+print(f"rank{dist.get_rank()} sum={x.item()} world={dist.get_world_size()}")
+open(f"rank{dist.get_rank()}.txt", "w").write(str(x.item()))
+dist.destroy_process_group()
+"""
+
+
+def test_rank_env():
+    env = rank_env(1, 4, [4, 5, 6, 7], 29500)
+    assert env["RANK"] == "1" and env["WORLD_SIZE"] == "4" and env["HIP_VISIBLE_DEVICES"] == "4,5,6,7"
+
+
+def test_gang_of_two_ranks_allreduce(tmp_path):
+    ensure_native_executor()
+
+    async def go():
+        ex = ExecutorProcess("gang", str(tmp_path / "sb"), gpus="", target=1)
+        await ex.start()
+        try:
+            await ex.wait_ready(1, 120)
+            resp = await ex.post(
+                "/v1/execute",
+                {"source_code": GANG, "nprocs": 2, "gpus": "", "timeout": 120, "collect_dir": str(tmp_path)},
+                timeout=200,
+            )
+            return resp.status_code, resp.json()
+        finally:
+            await ex.close()
+
+    status, body = asyncio.run(go())
+    assert status == 200, body
+    assert body["exit_code"] == 0, body["stderr"]
+    lines = sorted(body["stdout"].split())
+    assert "rank0" in body["stdout"] and "rank1" in body["stdout"]
+    assert "sum=3.0" in body["stdout"]
+    # both ranks share one workspace: both files come back
+    assert set(body["files"]) == {"/workspace/rank0.txt", "/workspace/rank1.txt"}
+
+
+def test_gang_reservation_blocks_and_releases(tmp_path):
+    ensure_native_executor()
+
+    async def go():
+        ex = ExecutorProcess("resv", str(tmp_path / "sb"), gpus="", target=1)
+        await ex.start()
+        try:
+            await ex.wait_ready(1, 120)
+            r = await ex.post("/v1/reserve", {"ttl": 30, "wait": 5})
+            assert r.status_code == 200 and r.json()["drained"]
+            # a normal job waits while the reservation holds ...
+            job = asyncio.ensure_future(ex.post("/v1/execute", {"source_code": "print(7)"}, timeout=60))
+            await asyncio.sleep(0.5)
+            assert not job.done()
+            # ... a gang job bypasses it ...
+            g = await ex.post("/v1/execute", {"source_code": "print(8)", "gang": True}, timeout=60)
+            assert g.json()["stdout"] == "8\n"
+            # ... and release lets the queued job through
+            await ex.post("/v1/release", {})
+            done = await asyncio.wait_for(job, 30)
+            return done.json()
+        finally:
+            await ex.close()
+
+    out = asyncio.run(go())
+    assert out["stdout"] == "7\n"

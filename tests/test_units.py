@@ -1,0 +1,314 @@
+"""Unit tests of the pure-Python layers (no executor, no GPU)."""
+
+import asyncio
+import json
+import os
+
+import pytest
+
+from bee_code_interpreter_fs_amd.config import Config
+from bee_code_interpreter_fs_amd.models import proto as pb
+from bee_code_interpreter_fs_amd.services.custom_tool_executor import (
+    CustomToolParseError,
+    annotation_to_schema,
+    build_tool_script,
+    parse_docstring,
+    parse_tool,
+)
+from bee_code_interpreter_fs_amd.services.metrics import Metrics
+from bee_code_interpreter_fs_amd.services.multipart import MultipartError, boundary_of, parse_multipart
+from bee_code_interpreter_fs_amd.services.storage import Storage
+from bee_code_interpreter_fs_amd.utils.retry import async_retry, backoff_delays
+from bee_code_interpreter_fs_amd.utils.validation import (
+    ValidationError,
+    check_file_map,
+    is_absolute_path,
+    is_hash,
+    resolve_logical_path,
+    split_logical_path,
+)
+
+# ---------------------------------------------------------------- config --
+
+
+def test_config_defaults_match_reference():
+    c = Config(_env={})
+    assert c.grpc_listen_addr == "0.0.0.0:50051"
+    assert c.http_listen_addr == "0.0.0.0:8000"
+    assert c.executor_image == "localhost/bee-code-executor:local"
+    assert c.executor_container_resources == {} and c.executor_pod_spec_extra == {}
+    assert c.file_storage_path == "./.tmp/files"
+    assert c.executor_pod_queue_target_length == 5
+    assert c.executor_pod_name_prefix == "code-executor-"
+    assert c.grpc_tls_cert is None
+    fmt = c.logging_config["formatters"]["standard"]["format"]
+    assert fmt == "[%(levelname)s] [%(request_id)s] %(name)s: %(message)s"
+
+
+def test_config_env_parsing():
+    env = {
+        "APP_GRPC_LISTEN_ADDR": "127.0.0.1:1",
+        "app_executor_pod_queue_target_length": "9",  # case-insensitive
+        "APP_EXECUTOR_CONTAINER_RESOURCES": '{"limits": {"amd.com/gpu": 1}}',
+        "APP_GRPC_TLS_CERT": "-----BEGIN CERT-----",
+        "APP_HTTP_LISTEN_ADDR": "",  # empty is ignored
+        "APP_GPU_IDS": "[0, 3]",
+        "APP_BROKER_ENABLED": "false",
+        "APP_DEFAULT_TIMEOUT": "12.5",
+        "OTHER": "x",
+    }
+    c = Config(_env=env)
+    assert c.grpc_listen_addr == "127.0.0.1:1"
+    assert c.executor_pod_queue_target_length == 9
+    assert c.executor_container_resources == {"limits": {"amd.com/gpu": 1}}
+    assert c.grpc_tls_cert == b"-----BEGIN CERT-----"
+    assert c.http_listen_addr == "0.0.0.0:8000"
+    assert c.gpu_ids == [0, 3]
+    assert c.broker_enabled is False
+    assert c.default_timeout == 12.5
+
+
+def test_config_rejects_bad_values():
+    with pytest.raises(ValueError):
+        Config(_env={"APP_EXECUTOR_POD_QUEUE_TARGET_LENGTH": "many"})
+    with pytest.raises(ValueError):
+        Config(_env={"APP_EXECUTOR_POD_SPEC_EXTRA": "[1, 2]"})
+    with pytest.raises(TypeError):
+        Config(_env={}, not_a_field=1)
+
+
+# ------------------------------------------------------------ validation --
+
+
+def test_hash_and_path_patterns():
+    assert is_hash("abc_DEF-123") and not is_hash("") and not is_hash("a/b") and not is_hash("x" * 256)
+    assert is_absolute_path("/workspace/a") and not is_absolute_path("//x") and not is_absolute_path("rel")
+
+
+@pytest.mark.parametrize(
+    "path,root,rel",
+    [
+        ("/workspace/a.txt", "/workspace", "a.txt"),
+        ("/workspace/d/e/f.csv", "/workspace", "d/e/f.csv"),
+        ("/runtime-packages/pkg/__init__.py", "/runtime-packages", "pkg/__init__.py"),
+        ("/data/x.bin", "/workspace", "data/x.bin"),
+    ],
+)
+def test_split_logical_path(path, root, rel):
+    assert split_logical_path(path) == (root, rel)
+
+
+@pytest.mark.parametrize("bad", ["/workspace/../etc/passwd", "/workspace/./a", "/workspace//a", "/workspace", "relative"])
+def test_traversal_rejected(bad):
+    with pytest.raises(ValidationError):
+        split_logical_path(bad)
+
+
+def test_resolve_logical_path(tmp_path):
+    ws, rp = str(tmp_path / "ws"), str(tmp_path / "rp")
+    assert resolve_logical_path("/workspace/a/b", ws, rp) == os.path.join(ws, "a/b")
+    assert resolve_logical_path("/runtime-packages/m.py", ws, rp) == os.path.join(rp, "m.py")
+
+
+def test_check_file_map_collects_errors():
+    with pytest.raises(ValidationError) as e:
+        check_file_map({"rel": "ok", "/workspace/x": "bad hash!", "/workspace/../y": "ok"})
+    assert len(e.value.errors) == 3
+
+
+# --------------------------------------------------------------- storage --
+
+
+def test_storage_roundtrip(tmp_path):
+    st = Storage(str(tmp_path / "s"))
+
+    async def go():
+        h = await st.write(b"hello")
+        assert len(h) == 64 and await st.exists(h)
+        assert await st.read(h) == b"hello"
+        async with st.writer() as w:
+            await w.write(b"a" * (3 << 20))
+            await w.write(b"b")
+        assert await st.size(w.hash) == (3 << 20) + 1
+        async with st.reader(w.hash) as r:
+            chunks = [c async for c in r.iter_chunks(1 << 20)]
+        assert b"".join(chunks)[-1:] == b"b"
+        await st.delete(h)
+        assert not await st.exists(h)
+        with pytest.raises(FileNotFoundError):
+            await st.delete(h)
+        with pytest.raises(FileNotFoundError):
+            await st.read("nope")
+        with pytest.raises(FileNotFoundError):
+            await st.read("../etc/passwd")
+
+    asyncio.run(go())
+
+
+def test_storage_adopt_links(tmp_path):
+    st = Storage(str(tmp_path / "s"))
+    src = tmp_path / "out.txt"
+    src.write_text("result")
+    oid = st.adopt_file(str(src))
+    assert open(st.path_of(oid)).read() == "result"
+
+
+def test_storage_failed_write_leaves_nothing(tmp_path):
+    st = Storage(str(tmp_path / "s"))
+
+    async def go():
+        with pytest.raises(RuntimeError):
+            async with st.writer() as w:
+                await w.write(b"partial")
+                raise RuntimeError("client went away")
+
+    asyncio.run(go())
+    assert [f for f in os.listdir(st.storage_path) if not f.startswith(".")] == []
+
+
+# ------------------------------------------------------------ custom tool --
+
+
+def test_docstring_sections():
+    desc, ret, params = parse_docstring(
+        """
+        Does things.
+        Second line: with a colon.
+
+        :param x: first
+          continued
+        :param y2: second
+        :returns: a thing
+        :raises ValueError: ignored
+        """
+    )
+    assert desc == "Does things.\nSecond line: with a colon."
+    assert params == {"x": "first\n  continued", "y2": "second"}
+    assert ret == "a thing"
+
+
+@pytest.mark.parametrize(
+    "ann,schema",
+    [
+        ("int", {"type": "integer"}),
+        ("typing.Optional[int]", {"anyOf": [{"type": "null"}, {"type": "integer"}]}),
+        ("list[float]", {"type": "array", "items": {"type": "number"}}),
+        ("dict[str, bool]", {"type": "object", "additionalProperties": {"type": "boolean"}}),
+        ("Tuple[int, str]", {"type": "array", "minItems": 2, "items": [{"type": "integer"}, {"type": "string"}], "additionalItems": False}),
+        ("int | None", {"anyOf": [{"type": "integer"}, {"type": "null"}]}),
+        ("Any", {}),
+    ],
+)
+def test_annotation_mapping(ann, schema):
+    import ast
+
+    assert annotation_to_schema(ast.parse(ann, mode="eval").body) == schema
+
+
+def test_parse_errors():
+    with pytest.raises(CustomToolParseError) as e:
+        parse_tool("def f(:\n  pass")
+    assert e.value.errors[0].startswith("Syntax error:")
+    with pytest.raises(CustomToolParseError) as e:
+        parse_tool("x = 1\ndef f(a: int):\n  pass")
+    assert "single function" in e.value.errors[0]
+    with pytest.raises(CustomToolParseError) as e:
+        parse_tool("def f(a: dict[int, str]):\n  pass")
+    assert "Unsupported type" in e.value.errors[0]
+    with pytest.raises(CustomToolParseError):
+        parse_tool("")
+
+
+def test_tool_script_runs_locally():
+    import subprocess
+    import sys
+
+    script = build_tool_script("import math\ndef hyp(a: float, b: float) -> float:\n  print('noise')\n  return math.hypot(a, b)", {"a": 3, "b": 4})
+    out = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True)
+    assert out.returncode == 0 and json.loads(out.stdout) == 5.0
+
+
+# ----------------------------------------------------------------- proto --
+
+
+def test_proto_roundtrip_and_oneof():
+    req = pb.ExecuteRequest(source_code="print(1)", executor_id="x", files={"/workspace/a": "h"}, gpus=2)
+    assert pb.ExecuteRequest.FromString(req.SerializeToString()) == req
+    r = pb.ParseCustomToolResponse(success={"tool_name": "t"})
+    assert r.WhichOneof("response") == "success"
+    r = pb.ExecuteCustomToolResponse(error={"stderr": "boom"})
+    assert r.WhichOneof("response") == "error" and r.error.stderr == "boom"
+    names = {m.name for m in pb.code_interpreter.descriptor.services_by_name["CodeInterpreterService"].methods}
+    assert names == {"Execute", "ParseCustomTool", "ExecuteCustomTool"}
+
+
+# ------------------------------------------------------------- multipart --
+
+
+def test_multipart_streaming_parser():
+    boundary = "XyZ123"
+    body = (
+        f"--{boundary}\r\nContent-Disposition: form-data; name=\"other\"\r\n\r\nignored\r\n"
+        f"--{boundary}\r\nContent-Disposition: form-data; name=\"file\"; filename=\"a.bin\"\r\n"
+        "Content-Type: application/octet-stream\r\n\r\n"
+    ).encode() + b"\r\n--XyZ12 not a boundary\r\n" * 3 + f"\r\n--{boundary}--\r\n".encode()
+
+    async def chunks(n):
+        for i in range(0, len(body), n):
+            yield body[i : i + n]
+
+    for n in (1, 7, 64, 10_000):
+        got = {}
+
+        async def on_part(name, filename, headers):
+            got[name] = bytearray()
+
+            async def sink(data):
+                got[name] += data
+
+            return sink
+
+        parts = asyncio.run(parse_multipart(chunks(n), boundary, on_part))
+        assert parts == 2
+        assert bytes(got["other"]) == b"ignored"
+        assert bytes(got["file"]) == b"\r\n--XyZ12 not a boundary\r\n" * 3
+    assert boundary_of('multipart/form-data; boundary="abc"') == "abc"
+    with pytest.raises(MultipartError):
+        boundary_of("text/plain")
+
+
+# ------------------------------------------------------------ retry etc. --
+
+
+def test_retry_policy():
+    assert backoff_delays(3) == [4, 4]
+    assert backoff_delays(5, minimum=1, maximum=10) == [1, 2, 4, 8]
+    calls = []
+
+    async def nosleep(_):
+        return None
+
+    @async_retry((RuntimeError,), attempts=3, sleep=nosleep)
+    async def flaky():
+        calls.append(1)
+        if len(calls) < 3:
+            raise RuntimeError("transient")
+        return "ok"
+
+    assert asyncio.run(flaky()) == "ok" and len(calls) == 3
+
+    @async_retry((RuntimeError,), attempts=3, sleep=nosleep)
+    async def bad():
+        raise ValueError("not retried")
+
+    with pytest.raises(ValueError):
+        asyncio.run(bad())
+
+
+def test_metrics_render():
+    m = Metrics()
+    m.inc("bee_x_total", route="/a")
+    m.observe_ms("bee_lat_ms", 3.0, rpc="Execute")
+    text = m.render()
+    assert 'bee_x_total{route="/a"} 1.0' in text
+    assert 'bee_lat_ms_bucket{rpc="Execute",le="5"} 1' in text and "bee_lat_ms_count" in text
