@@ -91,6 +91,18 @@ def _targets() -> List[Target]:
                 link_flags=["-shared", "-fPIC", "-ldl", "-pthread"],
             )
         )
+    fm = os.path.join(CSRC, "fsmap")
+    if os.path.isdir(fm) and os.listdir(fm):
+        targets.append(
+            Target(
+                name="fsmap",
+                output=os.path.join(PKG, "lib", "libbee_fsmap.so"),
+                sources=sorted(os.path.join(fm, f) for f in os.listdir(fm) if f.endswith(".cpp")),
+                compiler=CXX,
+                compile_flags=["-O2", "-fPIC", "-std=c++17", "-Wall", "-U_FORTIFY_SOURCE", "-fvisibility=default"],
+                link_flags=["-shared", "-fPIC", "-ldl"],
+            )
+        )
     if os.path.isdir(rb) and os.listdir(rb):
         targets.append(
             Target(

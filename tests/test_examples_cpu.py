@@ -1,0 +1,149 @@
+"""The CPU example payloads (examples/*.py) through the full service stack,
+the way the reference's e2e suite drives its examples, plus
+the ``code_interpreter`` compatibility entry points.  GPU payloads
+(benchmark_numpy_gpu, beekern_kernels, torch_on_gpu, allreduce_gang) are
+exercised in tests/test_sandbox_gpu.py on the MI355X box.
+"""
+
+import os
+import subprocess
+import sys
+
+import grpc
+import pytest
+
+from bee_code_interpreter_fs_amd.models import proto as pb
+
+from .harness import ServiceHarness, ensure_native_executor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXAMPLES = os.path.join(ROOT, "examples")
+
+
+def src(name: str) -> str:
+    with open(os.path.join(EXAMPLES, name)) as fh:
+        return fh.read()
+
+
+@pytest.fixture(scope="module")
+def stub(tmp_path_factory):
+    ensure_native_executor()
+    h = ServiceHarness(str(tmp_path_factory.mktemp("svc")), default_timeout=60.0)
+    h.start()
+    channel = grpc.insecure_channel(h.grpc_target)
+    yield pb.CodeInterpreterServiceStub(channel)
+    channel.close()
+    h.stop()
+
+
+def run(stub, name, **kw):
+    return stub.Execute(pb.ExecuteRequest(source_code=src(name), **kw), timeout=120)
+
+
+def test_hello_world(stub):
+    r = run(stub, "hello_world.py")
+    assert (r.exit_code, r.stdout) == (0, "hello world\n")
+
+
+def test_write_then_read_file(stub):
+    w = run(stub, "write_file.py")
+    assert w.exit_code == 0 and set(w.files) == {"/workspace/greeting.txt"}
+    r = run(stub, "read_file.py", files=dict(w.files))
+    assert r.exit_code == 0 and r.stdout == "Hello, World!\n" and not r.files
+
+
+def test_workspace_layout(stub):
+    w = run(stub, "write_file.py")
+    r = run(stub, "workspace_layout.py", files=dict(w.files))
+    assert r.stdout.startswith("cwd: /workspace\n"), r.stdout
+    assert "greeting.txt" in r.stdout
+
+
+def test_shell_quoting_is_literal(stub):
+    r = run(stub, "shell_quoting.py")
+    assert r.exit_code == 0
+    assert r.stdout.splitlines() == [
+        "single 'quoted' text",
+        'double "quoted" text',
+        "literal $HOME and ${PATH}",
+        "back\\slash",
+    ]
+
+
+def test_division_error(stub):
+    r = run(stub, "division_error.py")
+    assert r.exit_code == 1 and "ZeroDivisionError" in r.stderr
+
+
+def test_scientific_stack(stub):
+    r = run(stub, "scientific_stack.py")
+    assert r.exit_code == 0 and "P-Value" in r.stdout, r.stderr
+
+
+def test_benchmark_fib(stub):
+    r = run(stub, "benchmark_fib.py")
+    assert r.exit_code == 0, r.stderr
+    assert "digits: 2090" in r.stdout and "Execution Time" in r.stdout
+
+
+def test_fib_recursive_hits_timeout(stub):
+    r = run(stub, "fib_recursive.py", timeout=1.0)
+    assert r.exit_code == -1 and "Execution timed out" in r.stderr
+    assert r.stdout == ""  # reference shape: ("", "Execution timed out", -1), server.rs:201-218
+
+
+def test_outbound_socket_reports_outcome(stub):
+    r = run(stub, "outbound_socket.py")
+    assert r.exit_code == 0
+    assert r.stdout.startswith("no egress") or r.stdout.startswith("b'HTTP")
+
+
+def test_compat_entry_points_import():
+    from code_interpreter.config import Config
+
+    assert Config().grpc_listen_addr
+    out = subprocess.run(
+        [sys.executable, "-c", "import code_interpreter.health_check as h; print(h.health_check.__name__)"],
+        cwd=ROOT, capture_output=True, text=True, timeout=120,
+    )
+    assert out.returncode == 0 and out.stdout.strip() == "health_check", out.stderr
+
+
+def test_absolute_workspace_paths(stub):
+    code = (
+        "import os, subprocess, sys\n"
+        "open('/workspace/out.txt', 'w').write('x')\n"
+        "os.makedirs('/workspace/d', exist_ok=True)\n"
+        "open('/workspace/d/y.txt', 'w').write('y')\n"
+        "print(os.getcwd(), sorted(os.listdir('/workspace')))\n"
+        "print(subprocess.run(['cat', '/workspace/d/y.txt'], capture_output=True, text=True).stdout)\n"
+        "print(__file__)\n"
+    )
+    r = stub.Execute(pb.ExecuteRequest(source_code=code), timeout=60)
+    assert r.exit_code == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[0].startswith("/workspace [") and "'out.txt'" in lines[0]
+    assert lines[1] == "y"
+    assert lines[-1].endswith(".py")
+    assert set(r.files) == {"/workspace/out.txt", "/workspace/d/y.txt"} or set(r.files) == {"/workspace/out.txt"}
+
+
+def test_source_file_traceback_names_workspace_path(tmp_path_factory):
+    """HTTP source_file: the script lives in the workspace, and the user sees
+    it under /workspace (tracebacks, __file__), as in a reference pod."""
+    import httpx
+
+    ensure_native_executor()
+    h = ServiceHarness(str(tmp_path_factory.mktemp("svc2")), default_timeout=60.0)
+    h.start()
+    try:
+        with httpx.Client(base_url=h.http_base, timeout=60) as http:
+            up = http.put("/v1/files", files={"file": ("div.py", src("division_error.py").encode())})
+            sid = up.json()["hash"]
+            body = http.post(
+                "/v1/execute", json={"source_file": "/workspace/tools/div.py", "files": {"/workspace/tools/div.py": sid}}
+            ).json()
+    finally:
+        h.stop()
+    assert body["exit_code"] == 1
+    assert 'File "/workspace/tools/div.py", line 3' in body["stderr"], body["stderr"]
