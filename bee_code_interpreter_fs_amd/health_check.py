@@ -39,9 +39,13 @@ def health_check(config: Config = None, target: str = None, timeout: float = 999
     assert response.stdout == "42\n", f"unexpected health-check output: {response.stdout!r} / {response.stderr!r}"
 
 
-if __name__ == "__main__":
+def main() -> None:
     try:
         health_check()
     except Exception as e:  # noqa: BLE001
         print(f"health check failed: {e}", file=sys.stderr)
         sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

@@ -38,6 +38,35 @@ sys.path.insert(0, ROOT)
 PAYLOAD = os.path.join(ROOT, "examples", "benchmark_numpy_gpu.py")
 EXPECTED = 10**8 / 3  # E[sum U^2]
 
+# BASELINE.json configs; "numpy_gpu" is the headline (metric + config the
+# driver records), the others are reported by tools/bench_suite.py.
+WORKLOADS = {
+    "numpy_gpu": (
+        "examples/benchmark_numpy_gpu.py",
+        "Execute RPCs/sec (benchmark-numpy payload via HIP kernels)",
+        "benchmark-numpy.py payload: 1e8 f64 rand+square+sum + 4096^3 bf16 GEMM per Execute",
+        "float64 (rand/square/sum) + bf16 (GEMM)",
+    ),
+    "numpy_cpu": (
+        "examples/benchmark_numpy_cpu.py",
+        "Execute RPCs/sec (unmodified benchmark-numpy payload, numpy on CPU)",
+        "benchmark-numpy.py payload: 1e8 f64 numpy rand+square+sum per Execute",
+        "float64",
+    ),
+    "fib": (
+        "examples/benchmark_fib.py",
+        "Execute RPCs/sec (benchmark-fib payload, GPU-pinned executor)",
+        "benchmark-fib.py payload: 1000 x fib(10000) Python bigint per Execute",
+        "python int",
+    ),
+    "hello": (
+        "examples/hello_world.py",
+        "Execute RPCs/sec (hello_world plumbing)",
+        "hello_world payload: print per Execute",
+        "n/a",
+    ),
+}
+
 
 def parse_args():
     p = argparse.ArgumentParser()
@@ -47,7 +76,9 @@ def parse_args():
     p.add_argument("--concurrency", type=int, default=8, help="closed-loop clients per GPU")
     p.add_argument("--pool-target", type=int, default=16, help="warm light sandboxes per GPU")
     p.add_argument("--frontends", type=int, default=0, help="front-end replicas (0 = one per GPU)")
-    p.add_argument("--payload", default=PAYLOAD)
+    p.add_argument("--workload", choices=sorted(WORKLOADS), default="numpy_gpu")
+    p.add_argument("--payload", default=None, help="override the workload's script")
+    p.add_argument("--cpu-only", action="store_true", help="executors without GPUs (BASELINE config 1)")
     p.add_argument("--no-gang-check", action="store_true")
     return p.parse_args()
 
@@ -89,7 +120,9 @@ def start_service(tmp: str, n_gpus: int, args):
             "APP_HTTP_LISTEN_ADDR": f"127.0.0.1:{hport}",
             # one executor per physical GPU (a rehearsal with more ranks than
             # GPUs folds the extra ranks onto the existing devices)
-            "APP_GPU_IDS": json.dumps(sorted({i % visible_gpus() for i in range(n_gpus)})),
+            "APP_GPU_IDS": json.dumps(sorted({i % visible_gpus() for i in range(n_gpus)}))
+            if not args.cpu_only
+            else "[]",
             "APP_FILE_STORAGE_PATH": os.path.join(tmp, "files"),
             "APP_SANDBOX_ROOT": os.path.join(tmp, "sandboxes"),
             "APP_WORKERS_PER_GPU_TARGET": "1",  # direct sandboxes: the payload does not need them
@@ -133,13 +166,14 @@ async def client_loop(target, pb, source, n, out):
             lat.append((time.perf_counter() - t) * 1e3)
             for k, v in r.timings_ms.items():
                 phases.setdefault(k, []).append(v)
-            ok = r.exit_code == 0 and "Result:" in r.stdout
-            if ok:
-                try:
+            ok = r.exit_code == 0
+            try:
+                if ok and "Result:" in r.stdout:  # benchmark-numpy payloads: check the math
                     ok = abs(float(r.stdout.split("Result:")[1].split()[0]) - EXPECTED) < 5e4
+                if ok and "Execution Time:" in r.stdout:
                     exec_times.append(float(r.stdout.split("Execution Time:")[1].split()[0]) * 1e3)
-                except (IndexError, ValueError):
-                    ok = False
+            except (IndexError, ValueError):
+                ok = False
             if not ok:
                 errors.append(f"exit={r.exit_code} stdout={r.stdout[-200:]!r} stderr={r.stderr[-500:]!r}")
 
@@ -210,14 +244,18 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
-    torch.cuda.set_device(local % visible_gpus())
+    has_gpu = torch.cuda.is_available()
+    if has_gpu:
+        torch.cuda.set_device(local % visible_gpus())
 
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        if has_gpu:
+            torch.cuda.synchronize()
 
-    source = open(args.payload).read()
+    script, metric, model, dtype = WORKLOADS[args.workload]
+    source = open(args.payload or os.path.join(ROOT, script)).read()
     loop = asyncio.new_event_loop()
     proc = None
     tmp = tempfile.mkdtemp(prefix="bee-bench-", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
@@ -252,10 +290,14 @@ def main():
             for g in gathered:
                 for k, v in g[4].items():
                     all_phases.setdefault(k, []).extend(v)
-            gang = gang_allreduce_check(target, n_gpus) if n_gpus > 1 and not args.no_gang_check else None
+            gang = (
+                gang_allreduce_check(target, n_gpus)
+                if n_gpus > 1 and not args.no_gang_check and not args.cpu_only
+                else None
+            )
             total = len(all_lat)
             out = {
-                "metric": "Execute RPCs/sec (benchmark-numpy payload via HIP kernels)",
+                "metric": metric,
                 "value": round(total / max_elapsed, 3) if max_elapsed > 0 else 0.0,
                 "unit": "requests/s",
                 "n_gpus": n_gpus,
@@ -265,13 +307,15 @@ def main():
                 "higher_is_better": True,
                 "scaling": "weak",
                 "vs_baseline": None,
-                "dtype": "float64 (rand/square/sum) + bf16 (GEMM)",
-                "data": "synthetic (device Philox RNG; random bf16 GEMM operands)",
+                "dtype": dtype,
+                "data": "synthetic (device Philox RNG; random bf16 GEMM operands)"
+                if args.workload == "numpy_gpu"
+                else "synthetic (the payload generates its own inputs)",
                 "config": {
-                    "model": "benchmark-numpy.py payload: 1e8 f64 rand+square+sum + 4096^3 bf16 GEMM per Execute",
+                    "model": model,
                     "global_batch": args.concurrency * world,
                     "seq_len": None,
-                    "parallelism": f"{n_gpus} GPU-pinned executor pods, {frontends} front-end replicas, "
+                    "parallelism": f"{n_gpus} {'CPU-only' if args.cpu_only else 'GPU-pinned'} executor pods, {frontends} front-end replicas, "
                     f"{args.concurrency * world} concurrent clients",
                 },
                 "p50_latency_ms": round(statistics.median(all_lat), 3) if all_lat else None,

@@ -97,7 +97,9 @@ bool SandboxPool::start(std::string* err) {
   }
   // the zygote is forked+exec'd BEFORE this process touches HIP (broker init)
   const bool want_broker = !cfg_.broker_lib.empty() && !cfg_.gpus.empty() && !cfg_.pod_mode;
-  const int nz = 1 + (want_broker ? std::max(1, cfg_.light_zygotes) : 0);
+  // CPU-only pools use light (torch-free) sandboxes too, just without a broker
+  const bool cpu_light = cfg_.gpus.empty() && !cfg_.pod_mode && cfg_.light_target > 0 && cfg_.light_zygotes > 0;
+  const int nz = 1 + (want_broker || cpu_light ? std::max(1, cfg_.light_zygotes) : 0);
   for (int i = 0; i < nz; ++i) {
     auto z = std::make_unique<Zygote>();
     z->index = i;
@@ -114,6 +116,7 @@ bool SandboxPool::start(std::string* err) {
       err->clear();
     }
   }
+  light_ok_ = broker_ != nullptr || cpu_light;
   acceptor_thread_ = std::thread([this] { worker_acceptor(); });
   cleanup_thread_ = std::thread([this] { cleanup_loop(); });
   {
@@ -454,7 +457,7 @@ void SandboxPool::refill_locked() {
 }
 
 int SandboxPool::target_of(int kind) const {
-  if (kind == kLight) return broker_ ? cfg_.light_target : 0;
+  if (kind == kLight) return light_ok_ ? cfg_.light_target : 0;
   return cfg_.target;
 }
 
@@ -707,8 +710,8 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   std::string err;
   // light (broker-backed, no HIP in the sandbox) unless the request needs
   // its own HIP context (torch & co) or the daemon has no broker
-  const std::string mode = req["mode"].str_or(broker_ ? "light" : "direct");
-  const int kind = (mode == "light" && broker_) ? kLight : kDirect;
+  const std::string mode = req["mode"].str_or(light_ok_ ? "light" : "direct");
+  const int kind = (mode == "light" && light_ok_) ? kLight : kDirect;
   if (!dedicated) {
     auto w = acquire(kind, cfg_.acquire_timeout_s, &err);
     if (!w) return fail(503, err);

@@ -164,6 +164,7 @@ class SandboxPool {
   std::deque<std::shared_ptr<Worker>> ready_[2];  // by WorkerKind
   int spawning_[2] = {0, 0};
   std::unique_ptr<KernelBroker> broker_;
+  bool light_ok_ = false;  // light sandboxes available (broker up, or a CPU-only pool)
   int64_t jobs_ = 0;            // admitted jobs (guarded by mu_)
   bool reserved_ = false;       // a gang holds this GPU
   double reserved_until_ = 0;   // mono ms

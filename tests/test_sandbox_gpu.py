@@ -126,3 +126,37 @@ def test_concurrent_gpu_executions(gsvc):
 
     rs = gsvc.call(many(), timeout=300)
     assert all(r.exit_code == 0 and r.stdout.strip() == "0.33" for r in rs), [(r.stdout, r.stderr[-200:]) for r in rs]
+
+
+def _example(name):
+    import os
+
+    return open(os.path.join(os.path.dirname(__file__), "..", "examples", name)).read()
+
+
+def test_example_beekern_kernels(gsvc):
+    r = run(gsvc, _example("beekern_kernels.py"))
+    assert r.exit_code == 0, r.stderr
+    mean_sq = float(r.stdout.split("mean of squares:")[1].split()[0])
+    assert abs(mean_sq - 1 / 3) < 1e-3
+    assert "gemm shape: (1024, 1024)" in r.stdout
+
+
+def test_example_torch_on_gpu(gsvc):
+    r = run(gsvc, _example("torch_on_gpu.py"))
+    assert r.exit_code == 0, r.stderr
+    assert "MI355" in r.stdout or "AMD" in r.stdout or "gfx950" in r.stdout, r.stdout
+
+
+def test_example_allreduce_gang_single_gpu(gsvc):
+    r = run(gsvc, _example("allreduce_gang.py"), gpus=1)
+    assert r.exit_code == 0, r.stderr
+    assert "allreduce ok world=1 value=1.0" in r.stdout
+
+
+def test_workspace_view_in_gpu_sandbox(gsvc):
+    code = "import beekern as bk, numpy as np, os\nnp.save('/workspace/v.npy', bk.random.rand(1000).numpy())\nprint(os.getcwd(), np.load('/workspace/v.npy').shape)"
+    r = run(gsvc, code)
+    assert r.exit_code == 0, r.stderr
+    assert r.stdout.strip() == "/workspace (1000,)"
+    assert set(r.files) == {"/workspace/v.npy"}
