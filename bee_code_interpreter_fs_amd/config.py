@@ -119,6 +119,8 @@ class Config:
     wheelhouse: Optional[str] = None
     # fault injection: probability that spawning a sandbox fails (tests)
     fault_spawn_fail_rate: float = 0.0
+    # recycle warm sandboxes that waited longer than this (seconds, 0 = never)
+    worker_max_idle_s: float = 900.0
     # max bytes of stdout / stderr returned per execution
     max_output_bytes: int = 16 * 1024 * 1024
 

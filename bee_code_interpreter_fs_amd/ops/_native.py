@@ -102,6 +102,11 @@ def _declare(lib: ctypes.CDLL) -> None:
             [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_f, c_int, c_vp],
             c_int,
         ),
+        "bk_gemm_bf16_tn_variant": (
+            [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_f, c_int, c_int, c_vp],
+            c_int,
+        ),
+        "bk_gemm_bf16_pick": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int], c_int),
         "bk_transpose_bf16": ([c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),
     }
     for name, (args, res) in sig.items():

@@ -57,7 +57,9 @@ class ExecutorProcess:
         light_target: int = 0,
         broker: bool = False,
         light_zygotes: int = 2,
+        extra_args: Optional[List[str]] = None,
     ) -> None:
+        self.extra_args = list(extra_args or [])
         self.light_target = light_target
         self.light_zygotes = light_zygotes
         self.broker = broker
@@ -112,7 +114,7 @@ class ExecutorProcess:
             preload.append(interposer)
         if preload:
             cmd += ["--preload", ":".join(preload)]
-        return cmd
+        return cmd + self.extra_args
 
     async def start(self, timeout: float = 60.0) -> None:
         if not os.path.exists(self.binary):

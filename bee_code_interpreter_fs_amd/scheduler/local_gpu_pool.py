@@ -140,6 +140,7 @@ class LocalGpuPoolBackend(CodeExecutor):
             light_target=c.light_workers_per_gpu_target,
             broker=c.broker_enabled,
             light_zygotes=c.light_zygotes_per_gpu,
+            extra_args=["--max-idle", str(c.worker_max_idle_s)],
         )
 
     async def wait_ready(self, timeout: float = 300.0) -> None:

@@ -48,7 +48,9 @@ void usage() {
           "usage: bee-executor [--mode pool|pod] [--listen host:port|unix:/path] [--gpus 0] [--target N]\n"
           "                    [--sandbox-root DIR] [--python PY] [--warm-gpu 0|1] [--max-spawns N]\n"
           "                    [--timeout S] [--hbm-quota BYTES] [--recursive-scan 0|1] [--preload SO]\n"
-          "                    [--pythonpath P] [--max-output BYTES]\n");
+          "                    [--pythonpath P] [--max-output BYTES] [--max-idle S] [--acquire-timeout S]\n"
+          "                    [--broker-lib SO] [--light-target N] [--light-zygotes N] [--light-preload MODS]\n"
+          "                    [--workspace DIR] [--runtime-packages DIR] [--die-with-parent 0|1]\n");
 }
 
 bool resolve_pod_path(const PoolConfig& cfg, const std::string& url_path, std::string* real, std::string* err) {
@@ -106,6 +108,7 @@ int main(int argc, char** argv) {
     else if (a == "--max-spawns") cfg.max_concurrent_spawns = atoi(val().c_str());
     else if (a == "--timeout") cfg.default_timeout_s = atof(val().c_str());
     else if (a == "--acquire-timeout") cfg.acquire_timeout_s = atof(val().c_str());
+    else if (a == "--max-idle") cfg.max_idle_s = atof(val().c_str());
     else if (a == "--hbm-quota") cfg.default_hbm_quota = atoll(val().c_str());
     else if (a == "--recursive-scan") cfg.recursive_scan = val() != "0";
     else if (a == "--preload") cfg.zygote_preload = val();

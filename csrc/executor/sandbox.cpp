@@ -621,7 +621,38 @@ void SandboxPool::cleanup_loop() {
       }
     }
     if (stopping_) break;
+    if (cfg_.max_idle_s > 0 && !cfg_.pod_mode) recycle_idle();
   }
+}
+
+// Warm sandboxes that waited longer than --max-idle are replaced with fresh
+// ones, so a pool never serves a process whose state (HIP context, broker
+// session, imported modules' caches) has aged past that bound.
+void SandboxPool::recycle_idle() {
+  std::vector<std::shared_ptr<Worker>> old;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    const double cutoff = mono_ms() - cfg_.max_idle_s * 1e3;
+    for (auto& q : ready_) {
+      for (auto it = q.begin(); it != q.end();) {
+        if ((*it)->t_ready > 0 && (*it)->t_ready < cutoff) {
+          (*it)->state = WorkerState::Failed;  // the exit notification must not touch the queues
+          old.push_back(*it);
+          it = q.erase(it);
+        } else {
+          ++it;
+        }
+      }
+    }
+  }
+  if (old.empty()) return;
+  for (auto& w : old) {
+    destroy(w);
+    m_recycled_++;
+  }
+  BEE_INFO("recycled %zu idle sandbox(es)", old.size());
+  std::lock_guard<std::mutex> lk(mu_);
+  refill_locked();
 }
 
 SandboxPool::RunResult SandboxPool::run_in(const std::shared_ptr<Worker>& w, const RunSpec& spec) {
@@ -996,6 +1027,7 @@ std::string SandboxPool::metrics_text() {
   line("bee_executor_timeouts_total", "counter", (double)m_timeouts_.load());
   line("bee_executor_workers_spawned_total", "counter", (double)m_spawned_.load());
   line("bee_executor_worker_spawn_failures_total", "counter", (double)m_spawn_failed_.load());
+  line("bee_executor_idle_recycled_total", "counter", (double)m_recycled_.load());
   line("bee_executor_inflight", "gauge", (double)m_inflight_.load());
   line("bee_executor_ready_workers", "gauge", (double)(ready_[kDirect].size() + ready_[kLight].size()));
   line("bee_executor_ready_light_workers", "gauge", (double)ready_[kLight].size());

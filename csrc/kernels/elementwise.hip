@@ -64,21 +64,41 @@ struct alignas(16) Vec {
   T v[N];
 };
 
+constexpr int kEwUnroll = 4;  // 16-B loads in flight per lane before the first store
+
 template <typename T, int OP>
 __global__ __launch_bounds__(256) void unary_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n) {
   using E = Elem<T>;
   using V = Vec<T>;
-  constexpr int N = V::N;
+  constexpr int N = V::N, U = kEwUnroll;
   const int64_t nvec = n / N;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (int64_t i = tid; i < nvec; i += stride) {
-    V a = reinterpret_cast<const V*>(x)[i];
+  const V* xv = reinterpret_cast<const V*>(x);
+  V* yv = reinterpret_cast<V*>(y);
+  // block-contiguous chunks of U*256 vectors: each load instruction of a wave
+  // covers 1 KiB contiguous and a block's U instructions one 16 KiB span
+  const int64_t chunk = (int64_t)U * blockDim.x;
+  const int64_t nfull = nvec / chunk;
+  for (int64_t cb = blockIdx.x; cb < nfull; cb += gridDim.x) {
+    const int64_t base = cb * chunk + threadIdx.x;
+    V a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = xv[base + u * blockDim.x];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < N; ++j) a[u].v[j] = E::store(unary<OP>(E::load(a[u].v[j])));
+#pragma unroll
+    for (int u = 0; u < U; ++u) yv[base + u * blockDim.x] = a[u];
+  }
+  for (int64_t i = nfull * chunk + tid; i < nvec; i += stride) {
+    V a = xv[i];
 #pragma unroll
     for (int j = 0; j < N; ++j) a.v[j] = E::store(unary<OP>(E::load(a.v[j])));
-    reinterpret_cast<V*>(y)[i] = a;
+    yv[i] = a;
   }
-  for (int64_t i = nvec * N + tid; i < n; i += stride) y[i] = E::store(unary<OP>(E::load(x[i])));
+  for (int64_t k = nvec * N + tid; k < n; k += stride) y[k] = E::store(unary<OP>(E::load(x[k])));
 }
 
 // y = op(a, b) with b an array (B_SCALAR=false) or a scalar (B_SCALAR=true);
@@ -90,26 +110,47 @@ __global__ __launch_bounds__(256) void binary_kernel(const T* __restrict__ a, co
   using C = typename E::C;
   using V = Vec<T>;
   constexpr int N = V::N;
+  constexpr int U = kEwUnroll;
   const C sc = (C)s;
   const int64_t nvec = n / N;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (int64_t i = tid; i < nvec; i += stride) {
-    V va = reinterpret_cast<const V*>(a)[i];
-    V vb;
-    if constexpr (!B_SCALAR) vb = reinterpret_cast<const V*>(b)[i];
+  const V* av = reinterpret_cast<const V*>(a);
+  const V* bv = reinterpret_cast<const V*>(b);
+  V* yv = reinterpret_cast<V*>(y);
+  auto apply = [&](V& va, const V& vb) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const C lhs = E::load(va.v[j]);
       const C rhs = B_SCALAR ? sc : E::load(vb.v[j]);
       va.v[j] = E::store(REVERSED ? binary<OP>(rhs, lhs) : binary<OP>(lhs, rhs));
     }
-    reinterpret_cast<V*>(y)[i] = va;
+  };
+  const int64_t chunk = (int64_t)U * blockDim.x;
+  const int64_t nfull = nvec / chunk;
+  for (int64_t cb = blockIdx.x; cb < nfull; cb += gridDim.x) {
+    const int64_t base = cb * chunk + threadIdx.x;
+    V va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      va[u] = av[base + u * blockDim.x];
+      if constexpr (!B_SCALAR) vb[u] = bv[base + u * blockDim.x];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) apply(va[u], vb[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) yv[base + u * blockDim.x] = va[u];
   }
-  for (int64_t i = nvec * N + tid; i < n; i += stride) {
-    const C lhs = E::load(a[i]);
-    const C rhs = B_SCALAR ? sc : E::load(b[i]);
-    y[i] = E::store(REVERSED ? binary<OP>(rhs, lhs) : binary<OP>(lhs, rhs));
+  for (int64_t i = nfull * chunk + tid; i < nvec; i += stride) {
+    V va = av[i], vb;
+    if constexpr (!B_SCALAR) vb = bv[i];
+    apply(va, vb);
+    yv[i] = va;
+  }
+  for (int64_t k = nvec * N + tid; k < n; k += stride) {
+    const C lhs = E::load(a[k]);
+    const C rhs = B_SCALAR ? sc : E::load(b[k]);
+    y[k] = E::store(REVERSED ? binary<OP>(rhs, lhs) : binary<OP>(lhs, rhs));
   }
 }
 

@@ -244,6 +244,10 @@ __global__ __launch_bounds__(256) void transpose_bf16(const uint16_t* __restrict
   }
 }
 
+bool gemm256_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16);  // gemm_bf16_256.hip
+void launch_gemm256(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
+                    float beta, bool out_bf16, hipStream_t stream);
+
 }  // namespace bk
 
 using namespace bk;
@@ -254,15 +258,25 @@ BK_API int bk_gemm_bf16_fast_ok(int M, int N, int K, int lda, int ldb) {
   return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % BN == 0 && K % BK == 0 && lda % 8 == 0 && ldb % 8 == 0;
 }
 
-// C = alpha * A . Bt^T + beta * C.  out_dtype: kBF16 or kF32.
-BK_API int bk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-                           float alpha, float beta, int out_dtype, hipStream_t stream) {
+// Kernel choice: the 256x256 phase-pipelined kernel when the shape fills at
+// least half the chip with 256^2 tiles, the 128x128 kernel for smaller
+// aligned shapes (4x the blocks), the guarded generic kernel otherwise.
+// variant: 0 = auto, 1 = generic, 2 = 128x128, 3 = 256x256 (benchmarks).
+BK_API int bk_gemm_bf16_tn_variant(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb,
+                                   int ldc, float alpha, float beta, int out_dtype, int variant, hipStream_t stream) {
   if (!A || !Bt || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N) return kBadArgument;
   if (out_dtype != kBF16 && out_dtype != kF32) return kBadArgument;
-  const bool fast = bk_gemm_bf16_fast_ok(M, N, K, lda, ldb) && aligned16(A) && aligned16(Bt);
-  if (fast) {
+  const bool al = aligned16(A) && aligned16(Bt);
+  const bool ok128 = al && bk_gemm_bf16_fast_ok(M, N, K, lda, ldb);
+  const bool ok256 = al && aligned16(C) && gemm256_ok(M, N, K, lda, ldb, ldc, out_dtype == kBF16);
+  if (variant == 0) variant = (ok256 && (M / 256) * (N / 256) >= 128) ? 3 : ok128 ? 2 : 1;
+  if ((variant == 3 && !ok256) || (variant == 2 && !ok128)) return kBadArgument;
+  const bool bf = out_dtype == kBF16;
+  if (variant == 3) {
+    launch_gemm256(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, bf, stream);
+  } else if (variant == 2) {
     const unsigned grid = (unsigned)((M / BM) * (N / BN));
-    if (out_dtype == kBF16)
+    if (bf)
       gemm_bf16_tn_fast<true><<<grid, kGemmThreads, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N, K,
                                                                  lda, ldb, ldc, alpha, beta);
     else
@@ -270,7 +284,7 @@ BK_API int bk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N,
                                                                   K, lda, ldb, ldc, alpha, beta);
   } else {
     dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
-    if (out_dtype == kBF16)
+    if (bf)
       gemm_bf16_tn_generic<true><<<grid, 256, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N, K, lda,
                                                            ldb, ldc, alpha, beta);
     else
@@ -278,6 +292,21 @@ BK_API int bk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N,
                                                             ldb, ldc, alpha, beta);
   }
   return launch_status();
+}
+
+// Which kernel `variant 0` resolves to for these operands (diagnostics).
+BK_API int bk_gemm_bf16_pick(const void* A, const void* Bt, const void* C, int M, int N, int K, int lda, int ldb,
+                             int ldc, int out_dtype) {
+  const bool al = aligned16(A) && aligned16(Bt);
+  const bool ok128 = al && bk_gemm_bf16_fast_ok(M, N, K, lda, ldb);
+  const bool ok256 = al && aligned16(C) && gemm256_ok(M, N, K, lda, ldb, ldc, out_dtype == kBF16);
+  return (ok256 && (M / 256) * (N / 256) >= 128) ? 3 : ok128 ? 2 : 1;
+}
+
+// C = alpha * A . Bt^T + beta * C.  out_dtype: kBF16 or kF32.
+BK_API int bk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                           float alpha, float beta, int out_dtype, hipStream_t stream) {
+  return bk_gemm_bf16_tn_variant(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, out_dtype, 0, stream);
 }
 
 BK_API int bk_transpose_bf16(const void* in, void* out, int rows, int cols, int ld_in, int ld_out,

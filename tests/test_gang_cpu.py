@@ -83,3 +83,25 @@ def test_gang_reservation_blocks_and_releases(tmp_path):
 
     out = asyncio.run(go())
     assert out["stdout"] == "7\n"
+
+
+def test_idle_sandboxes_are_recycled(tmp_path):
+    """--max-idle: warm sandboxes older than the bound are replaced."""
+    ensure_native_executor()
+
+    async def go():
+        ex = ExecutorProcess("idle", str(tmp_path / "sb"), gpus="", target=1, extra_args=["--max-idle", "1"])
+        await ex.start()
+        try:
+            await ex.wait_ready(1, 120)
+            await asyncio.sleep(3.0)
+            metrics = (await ex.client.request("GET", "/metrics", None, 10)).text
+            r = await ex.post("/v1/execute", {"source_code": "print(5)"}, timeout=60)
+            return metrics, r.json()
+        finally:
+            await ex.close()
+
+    metrics, body = asyncio.run(go())
+    recycled = [l for l in metrics.splitlines() if l.startswith("bee_executor_idle_recycled_total")]
+    assert recycled and float(recycled[0].split()[-1]) >= 1, metrics
+    assert body["stdout"] == "5\n"

@@ -181,3 +181,30 @@ def test_torch_interop(gpu):
     assert float(gpu.sum(v)) == pytest.approx(float(t.sum().item()))
     back = gpu.to_torch(gpu.square(v))
     torch.testing.assert_close(back, t * t)
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("out", ["float32", "bfloat16"])
+def test_gemm_kernel_variants_with_beta(gpu, variant, out):
+    """Every GEMM kernel (generic / 128^2 / 256^2 phase-pipelined) against an
+    fp64 reference, including the beta * C read-modify-write epilogue."""
+    import torch
+
+    from bee_code_interpreter_fs_amd.ops import _native
+
+    M, N, K = 512, 768, 320
+    g = torch.Generator(device="cuda").manual_seed(variant)
+    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    bt = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    dt = torch.float32 if out == "float32" else torch.bfloat16
+    c0 = torch.empty(M, N, device="cuda", dtype=dt).uniform_(-1, 1, generator=g)
+    c = c0.clone()
+    rc = _native.lib().bk_gemm_bf16_tn_variant(
+        a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, N, 0.75, 0.5, 0 if out == "float32" else 2, variant,
+        torch.cuda.current_stream().cuda_stream,
+    )
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = 0.75 * (a.double() @ bt.double().T) + 0.5 * c0.double()
+    tol = 1e-3 if out == "float32" else 4e-2
+    assert (c.double() - ref).abs().max().item() < tol * max(1.0, ref.abs().max().item())

@@ -13,7 +13,7 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from bee_code_interpreter_fs_amd import ops as bk  # noqa: E402
 
 
@@ -85,6 +85,11 @@ def main():
         b = bk.random.uniform(-1, 1, (size, size), dtype="bfloat16")
         bt = b.T  # Bt view: kernel reads the buffer as [N, K]
         flops = 2 * size**3
+        c_probe = bk.empty((size, size), "bfloat16")
+        from bee_code_interpreter_fs_amd.ops import _native
+
+        emit(kernel="gemm dispatch", size=size, variant=_native.lib().bk_gemm_bf16_pick(
+            a.ptr, b.ptr, c_probe.ptr, size, size, size, size, size, size, 2), a_mod=a.ptr % 256, c_mod=c_probe.ptr % 256)
         ms, mn = timed(lambda: bk.gemm_bf16_tn(a, b, "bfloat16"), reps=20)
         emit(kernel=f"gemm_bf16_tn {size}^3", ms=ms, min_ms=mn, TFLOPs=flops / ms / 1e9, TFLOPs_best=flops / mn / 1e9)
         ms2, _ = timed(lambda: bk.matmul(a, b), reps=10)

@@ -1,0 +1,6 @@
+source tools/gpu_steps.sh
+step kbench 300 python tools/bench_kernels.py
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_kernels -o run -- python3 $GRAFT_REPO_ROOT/tools/bench_kernels.py > $GRAFT_REPO_ROOT/gpurun_out/prof_kernels.log 2>&1
+echo "[step] rocprof rc=$?"
+grep dispatch $GRAFT_REPO_ROOT/gpurun_out/prof_kernels.log
