@@ -45,12 +45,15 @@ class Target:
     shared: bool = True
     headers: List[str] = field(default_factory=list)
     hip: bool = False
+    optional: bool = False  # built only when named explicitly
 
 
 def _targets() -> List[Target]:
     k = os.path.join(CSRC, "kernels")
     ex = os.path.join(CSRC, "executor")
     q = os.path.join(CSRC, "hbm_quota")
+    ex_srcs = sorted(os.path.join(ex, f) for f in os.listdir(ex) if f.endswith(".cpp")) if os.path.isdir(ex) else []
+    ex_hdrs = sorted(os.path.join(ex, f) for f in os.listdir(ex) if f.endswith(".hpp")) if os.path.isdir(ex) else []
     rb = os.path.join(CSRC, "rccl_bench")
     targets = [
         Target(
@@ -91,6 +94,27 @@ def _targets() -> List[Target]:
                 link_flags=["-shared", "-fPIC", "-ldl", "-pthread"],
             )
         )
+    # host sanitizer builds of the executor (opt-in: `python -m
+    # bee_code_interpreter_fs_amd._build bee-executor-asan bee-executor-tsan`);
+    # the daemon is host code only, so these are ordinary g++ sanitizers
+    for san, flags in (("asan", ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-static-libasan"]),
+                       ("tsan", ["-fsanitize=thread", "-fno-omit-frame-pointer"])):
+        extra = ["-include", os.path.join(CSRC, "sanitize", "tsan_compat.hpp")] if san == "tsan" else []
+        if ex_srcs:
+            targets.append(
+                Target(
+                    name=f"bee-executor-{san}",
+                    output=os.path.join(ROOT, "build", "sanitize", f"bee-executor-{san}"),
+                    sources=ex_srcs,
+                    compiler=CXX,
+                    compile_flags=["-O1", "-g", "-std=c++17", "-pthread", f"-I{ROCM}/include",
+                                   "-D__HIP_PLATFORM_AMD__", *flags, *extra],
+                    link_flags=[*flags, "-pthread", f"-L{ROCM}/lib", "-lamdhip64", "-ldl", f"-Wl,-rpath,{ROCM}/lib"],
+                    shared=False,
+                    headers=ex_hdrs,
+                    optional=True,
+                )
+            )
     fm = os.path.join(CSRC, "fsmap")
     if os.path.isdir(fm) and os.listdir(fm):
         targets.append(
@@ -144,7 +168,8 @@ def _compile(t: Target, src: str) -> str:
 def build(targets: Sequence[str] = (), jobs: int = 0, verbose: bool = True) -> List[str]:
     if not shutil.which(HIPCC) and not os.path.exists(HIPCC):
         raise RuntimeError(f"hipcc not found at {HIPCC}")
-    chosen = [t for t in _targets() if not targets or t.name in targets]
+    every = _targets()
+    chosen = [t for t in every if t.name in targets] if targets else [t for t in every if not t.optional]
     jobs = jobs or min(8, os.cpu_count() or 4)
     built = []
     with cf.ThreadPoolExecutor(max_workers=jobs) as pool:
