@@ -9,6 +9,7 @@
 //    grid-stride loop over a grid capped at ~8 blocks per CU (G11).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 #include <utility>
@@ -43,8 +44,16 @@ inline int dtype_size(int dt) {
 }
 
 // grid for a memory-bound grid-stride kernel: enough blocks to fill every CU
-// several times over, never more than the work needs.
-inline unsigned stream_grid(int64_t work_items, int block, int max_blocks_per_cu = 8) {
+// many times over, never more than the work needs.  The default cap of 64
+// blocks/CU comes from tools/ew_sweep.py on MI355X (1e8 f64): square
+// 5.36 -> 5.59 TB/s, Philox 4.43 -> 4.98 TB/s going from 8 to 64 blocks/CU
+// -- the dispatcher keeps CUs fuller than a long grid-stride loop does.
+inline unsigned stream_grid(int64_t work_items, int block, int max_blocks_per_cu = 64) {
+  // BK_STREAM_BLOCKS_PER_CU overrides the cap (tuning sweeps, tools/ew_sweep.py)
+  if (const char* e = getenv("BK_STREAM_BLOCKS_PER_CU")) {
+    const int v = atoi(e);
+    if (v > 0) max_blocks_per_cu = v;
+  }
   int64_t need = (work_items + block - 1) / block;
   int64_t cap = (int64_t)kNumCU * max_blocks_per_cu;
   if (need < 1) need = 1;
