@@ -28,6 +28,7 @@ import asyncio
 import json
 import logging
 import os
+import sys
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -140,7 +141,8 @@ class LocalGpuPoolBackend(CodeExecutor):
             light_target=c.light_workers_per_gpu_target,
             broker=c.broker_enabled,
             light_zygotes=c.light_zygotes_per_gpu,
-            extra_args=["--max-idle", str(c.worker_max_idle_s)],
+            extra_args=["--max-idle", str(c.worker_max_idle_s), "--min-target", str(c.min_workers_per_gpu_target),
+                        "--min-zygotes", str(c.min_zygotes_per_gpu)],
         )
 
     async def wait_ready(self, timeout: float = 300.0) -> None:
@@ -410,7 +412,18 @@ def sandbox_mode(request: ExecuteRequest, storage: Storage) -> str:
             return "direct"
     from ..runtime.deps import imported_modules
 
-    return "direct" if DIRECT_GPU_MODULES.intersection(imported_modules(source or "")) else "light"
+    mods = imported_modules(source or "")
+    if DIRECT_GPU_MODULES.intersection(mods):
+        return "direct"
+    if all(m in MIN_MODULES or m in _STDLIB for m in mods):
+        return "min"  # numpy/beekern/stdlib only: the fast-forking minimal zygote
+    return "light"
+
+
+# what the minimal zygote preloads (plus the standard library, imported on
+# demand at stdlib speed)
+MIN_MODULES = frozenset({"numpy", "beekern", "bee_code_interpreter_fs_amd"})
+_STDLIB = frozenset(getattr(sys, "stdlib_module_names", ()))
 
 
 def _detail(resp) -> str:

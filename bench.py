@@ -74,7 +74,7 @@ def parse_args():
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--concurrency", type=int, default=8, help="closed-loop clients per GPU")
-    p.add_argument("--pool-target", type=int, default=16, help="warm light sandboxes per GPU")
+    p.add_argument("--pool-target", type=int, default=16, help="warm minimal sandboxes per GPU")
     p.add_argument("--frontends", type=int, default=0, help="front-end replicas (0 = one per GPU)")
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="numpy_gpu")
     p.add_argument("--payload", default=None, help="override the workload's script")
@@ -126,7 +126,9 @@ def start_service(tmp: str, n_gpus: int, args):
             "APP_FILE_STORAGE_PATH": os.path.join(tmp, "files"),
             "APP_SANDBOX_ROOT": os.path.join(tmp, "sandboxes"),
             "APP_WORKERS_PER_GPU_TARGET": "1",  # direct sandboxes: the payload does not need them
-            "APP_LIGHT_WORKERS_PER_GPU_TARGET": str(args.pool_target),
+            # the payloads import only beekern/numpy/stdlib -> minimal sandboxes
+            "APP_MIN_WORKERS_PER_GPU_TARGET": str(args.pool_target),
+            "APP_LIGHT_WORKERS_PER_GPU_TARGET": "4",
             "APP_MAX_INFLIGHT_PER_GPU": str(max(args.concurrency * 2, 8)),
             "APP_DEFAULT_TIMEOUT": "300",
             "APP_FRONTEND_PROCESSES": str(frontends),
