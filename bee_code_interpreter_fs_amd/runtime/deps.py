@@ -78,8 +78,10 @@ def install_missing(source: str, target_dir: str, wheelhouse: str = "", timeout:
     """Install missing imports from ``wheelhouse`` into ``target_dir``; returns
     the distributions attempted.  Failures are ignored, as in the reference."""
     wheelhouse = wheelhouse or os.environ.get("BEE_WHEELHOUSE", "")
+    if not wheelhouse or not os.path.isdir(wheelhouse):
+        return []  # nothing to install from: skip the parse and the path scans
     missing = missing_modules(imported_modules(source))
-    if not missing or not wheelhouse or not os.path.isdir(wheelhouse):
+    if not missing:
         return []
     dists = [IMPORT_TO_DIST.get(m, m) for m in missing]
     cmd = [

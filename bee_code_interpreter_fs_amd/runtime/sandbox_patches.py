@@ -138,7 +138,16 @@ class _PatchFinder(importlib.abc.MetaPathFinder):
         return None
 
 
+_INSTALLED = False
+
+
 def install() -> None:
+    """Idempotent: the zygote installs the patches once before forking, so a
+    worker's call is free (modules imported later go through the finder)."""
+    global _INSTALLED
+    if _INSTALLED:
+        return
+    _INSTALLED = True
     for name, patch in PATCHES.items():
         mod = sys.modules.get(name)
         if mod is not None:
