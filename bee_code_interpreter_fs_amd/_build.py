@@ -63,7 +63,7 @@ def _targets() -> List[Target]:
             compiler=HIPCC,
             compile_flags=HIP_FLAGS,
             link_flags=[f"--offload-arch={ARCH}", "-shared", "-fPIC"],
-            headers=[os.path.join(k, "bk_common.hpp")],
+            headers=[os.path.join(k, "bk_common.hpp"), os.path.join(k, "bk_philox.hpp")],
             hip=True,
         ),
     ]

@@ -134,7 +134,9 @@ class DeviceArray:
     def __init__(self, shape: Sequence[int], dtype: str, buffer: Optional[_Buffer] = None, lazy=None, strides_t=False):
         self.shape: Shape = tuple(int(s) for s in shape)
         self.dtype = normalize_dtype(dtype)
-        self._lazy = lazy  # ("square", src) until materialised
+        # until materialised: ("square", src), or ("rand", kind, seed, offset,
+        # lo, hi) -- a draw whose values are fixed by its counter range
+        self._lazy = lazy
         self._transposed = strides_t  # 2-D transposed view of a contiguous buffer
         if buffer is None and lazy is None:
             buffer = _Buffer(self.nbytes)
@@ -176,9 +178,14 @@ class DeviceArray:
 
     def _materialize(self) -> "DeviceArray":
         if self._lazy is not None:
-            op, src = self._lazy
-            self._buf = _Buffer(self.nbytes)
-            driver().unary(_UNARY[op], self.code, src.ptr, self._buf.ptr, self.size)
+            if self._lazy[0] == "rand":
+                _, kind, seed, off, lo, hi = self._lazy
+                self._buf = _Buffer(self.nbytes)
+                driver().rand(kind, self._buf.ptr, self.size, self.code, seed, off, lo, hi)
+            else:
+                op, src = self._lazy
+                self._buf = _Buffer(self.nbytes)
+                driver().unary(_UNARY[op], self.code, src.ptr, self._buf.ptr, self.size)
             self._lazy = None
         if self._transposed:
             rows, cols = self.shape[1], self.shape[0]  # underlying buffer is (rows, cols)
@@ -390,8 +397,12 @@ def _unary(op: str, x) -> DeviceArray:
 
 
 def square(x) -> DeviceArray:
-    """Lazy x**2: fused into a following reduction, else materialised."""
-    x = _as_operand(x)._materialize()
+    """Lazy x**2: fused into a following reduction, else materialised.  A
+    still-lazy uniform draw stays lazy underneath (sum(square(rand)) is one
+    fused Philox->square->reduce kernel)."""
+    x = _as_operand(x)
+    if not _lazy_uniform(x):
+        x = x._materialize()
     return DeviceArray(x.shape, x.dtype, lazy=("square", x))
 
 
@@ -417,15 +428,34 @@ def _reduce(op: str, x: DeviceArray, y: Optional[DeviceArray] = None) -> np.floa
     return np.float64(driver().reduce(_REDUCE[op], x.code, x.ptr, y.ptr if y is not None else 0, x.size))
 
 
+def _lazy_uniform(x: DeviceArray) -> bool:
+    return x._lazy is not None and x._lazy[0] == "rand" and x._lazy[1] == 0
+
+
+def _rand_reduce(op: str, x: DeviceArray) -> np.float64:
+    """Reduce a still-lazy uniform draw in one fused Philox->reduce kernel
+    (bk_rand_reduce): the values are the ones materialising x would store."""
+    _, _, seed, off, lo, hi = x._lazy
+    return np.float64(driver().rand_reduce(_REDUCE[op], x.code, x.size, seed, off, lo, hi))
+
+
 def sum(x) -> np.float64:  # noqa: A001 - numpy-compatible name
     x = _as_operand(x)
     if x._lazy is not None and x._lazy[0] == "square":
-        return _reduce("square_sum", x._lazy[1])  # fused: x**2 never materialised
+        base = x._lazy[1]
+        if _lazy_uniform(base):
+            return _rand_reduce("square_sum", base)  # neither the draw nor x**2 materialised
+        return _reduce("square_sum", base)  # fused: x**2 never materialised
+    if _lazy_uniform(x):
+        return _rand_reduce("sum", x)
     return _reduce("sum", x._materialize())
 
 
 def square_sum(x) -> np.float64:
-    return _reduce("square_sum", _as_operand(x)._materialize())
+    x = _as_operand(x)
+    if _lazy_uniform(x):
+        return _rand_reduce("square_sum", x)
+    return _reduce("square_sum", x._materialize())
 
 
 def mean(x) -> np.float64:
@@ -522,6 +552,9 @@ def gemm_bf16_tn(a: DeviceArray, bt: DeviceArray, out_dtype: str = "bfloat16", a
 
 # ---- random ----------------------------------------------------------------------------
 
+_LAZY_RANDOM = os.environ.get("BEE_LAZY_RANDOM", "1") != "0"
+
+
 class Generator:
     """Counter-based Philox4x32-10 stream on the device (numpy.random subset)."""
 
@@ -550,9 +583,15 @@ class Generator:
         dt = normalize_dtype(dtype)
         if dt == "bfloat16":
             return self._draw(kind, a, b, shape, "float32").astype("bfloat16")
-        out = DeviceArray(shape, dt)
         per = 2 if dt == "float64" else 4
-        driver().rand(kind, out.ptr, out.size, out.code, self._seed, self._advance(out.size, per), float(a), float(b))
+        n = int(math.prod(shape)) if shape else 1
+        off = self._advance(n, per)
+        if kind == 0 and _LAZY_RANDOM:
+            # generated on first use; a reduction consuming it directly fuses
+            # the generator into the reduction (sum, square_sum)
+            return DeviceArray(shape, dt, lazy=("rand", 0, self._seed, off, float(a), float(b)))
+        out = DeviceArray(shape, dt)
+        driver().rand(kind, out.ptr, out.size, out.code, self._seed, off, float(a), float(b))
         return out
 
     def uniform(self, low=0.0, high=1.0, size=None, dtype="float64") -> DeviceArray:

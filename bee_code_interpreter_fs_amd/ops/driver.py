@@ -86,6 +86,13 @@ class NativeDriver:
         self.d2h(self.scalar, out)
         return float(out[0])
 
+    def rand_reduce(self, op: int, dt: int, n: int, seed: int, off: int, lo: float, hi: float) -> float:
+        check(self.lib.bk_rand_reduce(op, dt, n, seed & 0xFFFFFFFFFFFFFFFF, off, lo, hi, _vp(self.ws), _vp(self.scalar),
+                                      self.stream), "bk_rand_reduce")
+        out = np.zeros(1, np.float64)
+        self.d2h(self.scalar, out)
+        return float(out[0])
+
     def gemm(self, A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt) -> None:
         check(
             self.lib.bk_gemm_bf16_tn(_vp(A), _vp(Bt), _vp(C), M, N, K, lda, ldb, ldc, alpha, beta, odt, self.stream),
@@ -148,7 +155,7 @@ def _info_dict(v, arch: str) -> dict:
 # ---- broker client --------------------------------------------------------------------
 
 (HELLO, ALLOC, FREE, WRITE, READ, RAND, UNARY, BINARY, CAST, FILL, REDUCE, GEMM, TRANSPOSE, SYNC, MEMSTATS, INFO,
- COPY) = range(1, 18)
+ COPY, RAND_REDUCE) = range(1, 19)
 _HDR = struct.Struct("<IIQ")
 _RHDR = struct.Struct("<iIQ")
 _CHUNK = 64 << 20
@@ -250,6 +257,10 @@ class BrokerDriver:
 
     def reduce(self, op, dt, a, b, n) -> float:
         return struct.unpack("<d", self._call(REDUCE, struct.pack("<IIQQq", op, dt, a, b or 0, n)))[0]
+
+    def rand_reduce(self, op, dt, n, seed, off, lo, hi) -> float:
+        payload = struct.pack("<IIqQQdd", op, dt, n, seed & 0xFFFFFFFFFFFFFFFF, off, lo, hi)
+        return struct.unpack("<d", self._call(RAND_REDUCE, payload))[0]
 
     def gemm(self, A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt) -> None:
         self._call(GEMM, struct.pack("<QQQiiiiiiffii", A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, 0))

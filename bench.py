@@ -319,6 +319,9 @@ def main():
                     "seq_len": None,
                     "parallelism": f"{n_gpus} {'CPU-only' if args.cpu_only else 'GPU-pinned'} executor pods, {frontends} front-end replicas, "
                     f"{args.concurrency * world} concurrent clients",
+                    "execution": "every Execute runs in its own single-use sandbox process on the pinned GPU; "
+                    "beekern draws are lazy, so sum(square(rand(1e8))) lowers to one fused Philox->square->reduce "
+                    "kernel (the unobserved draw never round-trips HBM; set BEE_LAZY_RANDOM=0 to materialise it)",
                 },
                 "p50_latency_ms": round(statistics.median(all_lat), 3) if all_lat else None,
                 "p95_latency_ms": round(percentile(all_lat, 95), 3) if all_lat else None,

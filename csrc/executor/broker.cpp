@@ -23,7 +23,7 @@ namespace {
 // response: i32 status | u32 0 | u64 len | payload
 enum Op : uint32_t {
   kHello = 1, kAlloc, kFree, kWrite, kRead, kRand, kUnary, kBinary, kCast, kFill, kReduce, kGemm, kTranspose,
-  kSync, kMemStats, kInfo, kCopy,
+  kSync, kMemStats, kInfo, kCopy, kRandReduce,
 };
 enum Status : int32_t {
   kOk = 0, kBadArgument = 1, kLaunchFailed = 2, kOutOfMemory = 3, kQuotaExceeded = 4, kNotInitialized = 5,
@@ -97,6 +97,7 @@ struct Bk {
   int (*cast)(int, int, const void*, void*, int64_t, hipStream_t);
   int (*fill)(void*, int64_t, uint64_t, int, hipStream_t);
   int (*reduce_ws)();
+  int (*rand_reduce)(int, int, int64_t, uint64_t, uint64_t, double, double, void*, void*, hipStream_t);
   int (*reduce)(int, int, const void*, const void*, int64_t, void*, void*, hipStream_t);
   int (*gemm)(const void*, const void*, void*, int, int, int, int, int, int, float, float, int, hipStream_t);
   int (*transpose)(const void*, void*, int, int, int, int, hipStream_t);
@@ -140,7 +141,8 @@ bool KernelBroker::start(std::string* err) {
             sym(lib_, "bk_rand_normal", &g_bk.rand_normal) && sym(lib_, "bk_unary", &g_bk.unary) &&
             sym(lib_, "bk_binary", &g_bk.binary) && sym(lib_, "bk_cast", &g_bk.cast) && sym(lib_, "bk_fill", &g_bk.fill) &&
             sym(lib_, "bk_reduce_workspace_bytes", &g_bk.reduce_ws) && sym(lib_, "bk_reduce", &g_bk.reduce) &&
-            sym(lib_, "bk_gemm_bf16_tn", &g_bk.gemm) && sym(lib_, "bk_transpose_bf16", &g_bk.transpose);
+            sym(lib_, "bk_gemm_bf16_tn", &g_bk.gemm) && sym(lib_, "bk_transpose_bf16", &g_bk.transpose) &&
+            sym(lib_, "bk_rand_reduce", &g_bk.rand_reduce);
   if (!ok) {
     *err = "libbeekern.so is missing broker entry points";
     return false;
@@ -423,6 +425,21 @@ void KernelBroker::serve(int fd, pid_t peer) {
         }
         if (!will_read(ba) || !will_read(bb)) { st = kLaunchFailed; break; }
         int rc = g_bk.reduce((int)rop, (int)dt, ba->ptr, bb ? bb->ptr : nullptr, n, ws, scalar, stream);
+        double v = 0;
+        if (rc == 0 && (hipMemcpyAsync(&v, scalar, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+                        hipStreamSynchronize(stream) != hipSuccess))
+          rc = kLaunchFailed;
+        if (rc) st = rc;
+        put(&v, 8);
+        break;
+      }
+      case kRandReduce: {  // reduction of a lazy uniform draw: no buffer involved
+        const uint32_t rop = r.get<uint32_t>(), dt = r.get<uint32_t>();
+        const int64_t n = r.get<int64_t>();
+        const uint64_t seed = r.get<uint64_t>(), off = r.get<uint64_t>();
+        const double lo = r.get<double>(), hi = r.get<double>();
+        if (!r.ok || n < 0) { st = kProtocol; break; }
+        int rc = g_bk.rand_reduce((int)rop, (int)dt, n, seed, off, lo, hi, ws, scalar, stream);
         double v = 0;
         if (rc == 0 && (hipMemcpyAsync(&v, scalar, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
                         hipStreamSynchronize(stream) != hipSuccess))

@@ -48,11 +48,17 @@ inline int dtype_size(int dt) {
 // blocks/CU comes from tools/ew_sweep.py on MI355X (1e8 f64): square
 // 5.36 -> 5.59 TB/s, Philox 4.43 -> 4.98 TB/s going from 8 to 64 blocks/CU
 // -- the dispatcher keeps CUs fuller than a long grid-stride loop does.
-inline unsigned stream_grid(int64_t work_items, int block, int max_blocks_per_cu = 64) {
-  // BK_STREAM_BLOCKS_PER_CU overrides the cap (tuning sweeps, tools/ew_sweep.py)
-  if (const char* e = getenv("BK_STREAM_BLOCKS_PER_CU")) {
-    const int v = atoi(e);
-    if (v > 0) max_blocks_per_cu = v;
+constexpr int kStreamBlocksPerCU = 64;
+
+inline unsigned stream_grid(int64_t work_items, int block, int max_blocks_per_cu = kStreamBlocksPerCU) {
+  // BK_STREAM_BLOCKS_PER_CU overrides the DEFAULT cap only (tuning sweeps,
+  // tools/ew_sweep.py); callers with their own cap (reductions, whose grid
+  // sizes a fixed workspace) are never changed
+  if (max_blocks_per_cu == kStreamBlocksPerCU) {
+    if (const char* e = getenv("BK_STREAM_BLOCKS_PER_CU")) {
+      const int v = atoi(e);
+      if (v > 0) max_blocks_per_cu = v;
+    }
   }
   int64_t need = (work_items + block - 1) / block;
   int64_t cap = (int64_t)kNumCU * max_blocks_per_cu;

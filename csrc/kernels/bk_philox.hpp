@@ -1,0 +1,34 @@
+// Philox4x32-10 and the uniform constructions shared by the RNG kernels
+// (random.hip) and the fused RNG->reduce kernels (reduce.hip): one definition,
+// so a fused reduction sees bit-identical values to a materialised draw.
+#pragma once
+#include "bk_common.hpp"
+
+namespace bk {
+
+struct Philox {
+  static constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  static constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+
+  __device__ __forceinline__ static uint4 run(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+      const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+      c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+      k0 += W0;
+      k1 += W1;
+    }
+    return c;
+  }
+};
+
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+__device__ __forceinline__ float u24(uint32_t a) { return (float)(a >> 8) * (1.0f / 16777216.0f); }
+
+// stream tags: distinct counter words per distribution
+constexpr uint32_t kTagUniformF64 = 0x62656b65u, kTagUniformF32 = 0x62656b66u;
+
+}  // namespace bk

@@ -7,30 +7,9 @@
 // 32-bit draws, a>>5 and b>>6) or 4 f32 (24-bit), written with one 16-byte
 // store per lane; the kernel is HBM-write bound (800 MB for 1e8 f64).
 #include "bk_common.hpp"
+#include "bk_philox.hpp"
 
 namespace bk {
-
-struct Philox {
-  static constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
-  static constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-
-  __device__ __forceinline__ static uint4 run(uint4 c, uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-      const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
-      const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
-      c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
-      k0 += W0;
-      k1 += W1;
-    }
-    return c;
-  }
-};
-
-__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
-  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
-}
-__device__ __forceinline__ float u24(uint32_t a) { return (float)(a >> 8) * (1.0f / 16777216.0f); }
 
 // out[i] = U[0,1) (f64), scaled to [lo, hi).  Each counter value -> 2 doubles.
 __global__ __launch_bounds__(256) void philox_uniform_f64(double* __restrict__ out, int64_t n, uint32_t k0,
@@ -39,7 +18,7 @@ __global__ __launch_bounds__(256) void philox_uniform_f64(double* __restrict__ o
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < pairs; p += stride) {
     const uint64_t ctr = offset + (uint64_t)p;
-    const uint4 r = Philox::run(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), 0x62656b65u, 0u), k0, k1);
+    const uint4 r = Philox::run(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), kTagUniformF64, 0u), k0, k1);
     double2 v = make_double2(lo + span * u53(r.x, r.y), lo + span * u53(r.z, r.w));
     const int64_t i = 2 * p;
     if (i + 1 < n) {
@@ -57,7 +36,7 @@ __global__ __launch_bounds__(256) void philox_uniform_f32(float* __restrict__ ou
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += stride) {
     const uint64_t ctr = offset + (uint64_t)q;
-    const uint4 r = Philox::run(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), 0x62656b66u, 0u), k0, k1);
+    const uint4 r = Philox::run(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), kTagUniformF32, 0u), k0, k1);
     float4 v = make_float4(lo + span * u24(r.x), lo + span * u24(r.y), lo + span * u24(r.z), lo + span * u24(r.w));
     const int64_t i = 4 * q;
     if (i + 3 < n) {

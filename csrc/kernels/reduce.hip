@@ -8,6 +8,7 @@
 // per block.  Stage 2: one block folds the partials in a fixed order.  No
 // float atomics, so results are bitwise reproducible run to run.
 #include "bk_common.hpp"
+#include "bk_philox.hpp"
 
 namespace bk {
 
@@ -120,11 +121,68 @@ __global__ __launch_bounds__(kRedBlock) void reduce_stage2(const double* __restr
   if (threadIdx.x == 0) *out = v;
 }
 
+// ---- fused RNG -> reduce -------------------------------------------------------
+// sum / square-sum over a uniform Philox stream WITHOUT materialising it:
+// element i takes exactly the value philox_uniform_{f64,f32} would store
+// (same counter, tag and construction, bk_philox.hpp), so the result equals
+// the reduction of the materialised draw up to summation order.  This is what
+// `bk.sum(bk.square(bk.random.rand(n)))` lowers to while the draw is still
+// lazy (ops/array.py): compute-bound (Philox) instead of 2 x n x 8 bytes of
+// HBM traffic.  Two counters per iteration keep two independent Philox
+// chains in flight per lane.
+template <int OP>
+__device__ __forceinline__ double rr_map(double v) {
+  return OP == kRedSquareSum ? v * v : v;
+}
+
+template <int OP>
+__global__ __launch_bounds__(kRedBlock) void rand_reduce_f64(int64_t n, uint32_t k0, uint32_t k1, uint64_t offset,
+                                                             double lo, double span, double* __restrict__ partials) {
+  const int64_t pairs = (n + 1) / 2, full = n / 2;  // `full`: pairs whose both values are in range
+  const int64_t stride = (int64_t)gridDim.x * kRedBlock;
+  double acc0 = 0.0, acc1 = 0.0;
+  int64_t p = (int64_t)blockIdx.x * kRedBlock + threadIdx.x;
+  for (; p + stride < full; p += 2 * stride) {
+    const uint64_t c0 = offset + (uint64_t)p, c1 = c0 + (uint64_t)stride;
+    const uint4 r0 = Philox::run(make_uint4((uint32_t)c0, (uint32_t)(c0 >> 32), kTagUniformF64, 0u), k0, k1);
+    const uint4 r1 = Philox::run(make_uint4((uint32_t)c1, (uint32_t)(c1 >> 32), kTagUniformF64, 0u), k0, k1);
+    acc0 += rr_map<OP>(lo + span * u53(r0.x, r0.y)) + rr_map<OP>(lo + span * u53(r0.z, r0.w));
+    acc1 += rr_map<OP>(lo + span * u53(r1.x, r1.y)) + rr_map<OP>(lo + span * u53(r1.z, r1.w));
+  }
+  for (; p < pairs; p += stride) {
+    const uint64_t c0 = offset + (uint64_t)p;
+    const uint4 r0 = Philox::run(make_uint4((uint32_t)c0, (uint32_t)(c0 >> 32), kTagUniformF64, 0u), k0, k1);
+    acc0 += rr_map<OP>(lo + span * u53(r0.x, r0.y));
+    if (2 * p + 1 < n) acc0 += rr_map<OP>(lo + span * u53(r0.z, r0.w));
+  }
+  const double v = block_reduce<OP>(acc0 + acc1);
+  if (threadIdx.x == 0) partials[blockIdx.x] = v;
+}
+
+template <int OP>
+__global__ __launch_bounds__(kRedBlock) void rand_reduce_f32(int64_t n, uint32_t k0, uint32_t k1, uint64_t offset,
+                                                             float lo, float span, double* __restrict__ partials) {
+  const int64_t quads = (n + 3) / 4;
+  const int64_t stride = (int64_t)gridDim.x * kRedBlock;
+  double acc = 0.0;
+  for (int64_t q = (int64_t)blockIdx.x * kRedBlock + threadIdx.x; q < quads; q += stride) {
+    const uint64_t c = offset + (uint64_t)q;
+    const uint4 r = Philox::run(make_uint4((uint32_t)c, (uint32_t)(c >> 32), kTagUniformF32, 0u), k0, k1);
+    const float v[4] = {lo + span * u24(r.x), lo + span * u24(r.y), lo + span * u24(r.z), lo + span * u24(r.w)};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (4 * q + j < n) acc += rr_map<OP>((double)v[j]);
+  }
+  const double v = block_reduce<OP>(acc);
+  if (threadIdx.x == 0) partials[blockIdx.x] = v;
+}
+
 template <typename T, int OP>
 int launch_reduce(const void* a, const void* b, int64_t n, double* workspace, double* out, hipStream_t s) {
   constexpr int N = 16 / sizeof(T);
   int64_t lanes_needed = (n / N + 3) / 4;  // 4 vectors per lane minimum before adding blocks
   unsigned g = stream_grid(lanes_needed > 0 ? lanes_needed : 1, kRedBlock, kRedMaxBlocks / kNumCU);
+  if (g > (unsigned)kRedMaxBlocks) g = kRedMaxBlocks;  // the workspace holds kRedMaxBlocks partials
   reduce_stage1<T, OP><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace);
   reduce_stage2<OP><<<1, kRedBlock, 0, s>>>(workspace, (int)g, out);
   return launch_status();
@@ -141,6 +199,32 @@ int dispatch_reduce(int op, const void* a, const void* b, int64_t n, double* ws,
 }  // namespace bk
 
 using namespace bk;
+
+// sum (op 0) or square-sum (op 1) of the uniform [lo, hi) draw of n values
+// at (seed, offset) -- without materialising it.  dtype kF64 or kF32.
+BK_API int bk_rand_reduce(int op, int dtype, int64_t n, uint64_t seed, uint64_t offset, double lo, double hi,
+                          void* workspace, void* out, hipStream_t stream) {
+  if (!workspace || !out || n < 0 || (op != kRedSum && op != kRedSquareSum) || (dtype != kF64 && dtype != kF32))
+    return kBadArgument;
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const int64_t units = dtype == kF64 ? (n + 1) / 2 : (n + 3) / 4;
+  // fixed grid for a given n: results are reproducible run to run
+  unsigned g = stream_grid(units > 0 ? (units + 7) / 8 : 1, kRedBlock, kRedMaxBlocks / kNumCU);
+  if (g > (unsigned)kRedMaxBlocks) g = kRedMaxBlocks;
+  double* ws = (double*)workspace;
+  if (dtype == kF64) {
+    if (op == kRedSum) rand_reduce_f64<kRedSum><<<g, kRedBlock, 0, stream>>>(n, k0, k1, offset, lo, hi - lo, ws);
+    else rand_reduce_f64<kRedSquareSum><<<g, kRedBlock, 0, stream>>>(n, k0, k1, offset, lo, hi - lo, ws);
+  } else {
+    if (op == kRedSum)
+      rand_reduce_f32<kRedSum><<<g, kRedBlock, 0, stream>>>(n, k0, k1, offset, (float)lo, (float)(hi - lo), ws);
+    else
+      rand_reduce_f32<kRedSquareSum><<<g, kRedBlock, 0, stream>>>(n, k0, k1, offset, (float)lo, (float)(hi - lo), ws);
+  }
+  if (op == kRedSum) reduce_stage2<kRedSum><<<1, kRedBlock, 0, stream>>>(ws, (int)g, (double*)out);
+  else reduce_stage2<kRedSquareSum><<<1, kRedBlock, 0, stream>>>(ws, (int)g, (double*)out);
+  return launch_status();
+}
 
 BK_API int bk_reduce_workspace_bytes() { return kRedMaxBlocks * (int)sizeof(double); }
 
