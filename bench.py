@@ -104,6 +104,26 @@ def visible_gpus() -> int:
     return max(torch.cuda.device_count(), 1)
 
 
+def cpu_usage_s():
+    """(seconds of CPU used by this container so far, source) -- cgroup v2,
+    cgroup v1 cpuacct, or the host's /proc/stat busy time as a fallback."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                if line.startswith("usage_usec"):
+                    return int(line.split()[1]) / 1e6, "cgroup2"
+    except OSError:
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpuacct/cpuacct.usage") as f:
+            return int(f.read()) / 1e9, "cgroup1"
+    except OSError:
+        pass
+    with open("/proc/stat") as f:
+        v = [int(x) for x in f.readline().split()[1:]]
+    return (sum(v) - v[3] - v[4]) / os.sysconf("SC_CLK_TCK"), "procstat"
+
+
 def free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -273,10 +293,12 @@ def main():
 
         loop.run_until_complete(run_clients(target, source, args.concurrency, args.warmup))  # warm every pool
         barrier()
+        cpu0, cpu_src = cpu_usage_s()
         t0 = time.perf_counter()
         lat, errors, exec_times, phases = loop.run_until_complete(run_clients(target, source, args.concurrency, args.steps))
         barrier()
         elapsed = time.perf_counter() - t0
+        cpu_busy = (cpu_usage_s()[0] - cpu0) / elapsed if elapsed > 0 else 0.0
 
         gathered = [(elapsed, lat, errors, exec_times, phases)]
         if world > 1:
@@ -335,6 +357,7 @@ def main():
             if gang is not None:
                 out["gang_allreduce"] = gang
             out["executors"] = executor_stats(hport)
+            out["cpu_cores_busy"] = {"value": round(cpu_busy, 2), "source": cpu_src}
             print(json.dumps(out), flush=True)
         if world > 1:
             dist.barrier()
