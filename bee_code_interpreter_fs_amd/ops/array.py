@@ -429,7 +429,8 @@ def _reduce(op: str, x: DeviceArray, y: Optional[DeviceArray] = None) -> np.floa
 
 
 def _lazy_uniform(x: DeviceArray) -> bool:
-    return x._lazy is not None and x._lazy[0] == "rand" and x._lazy[1] == 0
+    # fused reductions exist for the f64 / f32 streams (bf16 draws materialise)
+    return x._lazy is not None and x._lazy[0] == "rand" and x._lazy[1] == 0 and x.dtype != "bfloat16"
 
 
 def _rand_reduce(op: str, x: DeviceArray) -> np.float64:
@@ -581,9 +582,9 @@ class Generator:
     def _draw(self, kind: int, a: float, b: float, size, dtype) -> DeviceArray:
         shape = _shape_of(size)
         dt = normalize_dtype(dtype)
-        if dt == "bfloat16":
+        if dt == "bfloat16" and kind != 0:
             return self._draw(kind, a, b, shape, "float32").astype("bfloat16")
-        per = 2 if dt == "float64" else 4
+        per = 2 if dt == "float64" else 4  # bf16 uniforms are the f32 stream, rounded
         n = int(math.prod(shape)) if shape else 1
         off = self._advance(n, per)
         if kind == 0 and _LAZY_RANDOM:

@@ -148,6 +148,20 @@ bool KernelBroker::start(std::string* err) {
     return false;
   }
   const double t0 = mono_ms();
+  // how host threads wait for the GPU (stream syncs in read/reduce/free):
+  // blocking sync sleeps on an interrupt instead of spinning a core per
+  // waiting sandbox connection -- at ~2k requests/s per GPU those spins were
+  // most of the daemon's CPU.  BEE_BROKER_SYNC=spin|yield|auto|blocking.
+  {
+    unsigned flags = hipDeviceScheduleBlockingSync;
+    const char* m = getenv("BEE_BROKER_SYNC");
+    if (m && !strcmp(m, "spin")) flags = hipDeviceScheduleSpin;
+    else if (m && !strcmp(m, "yield")) flags = hipDeviceScheduleYield;
+    else if (m && !strcmp(m, "auto")) flags = hipDeviceScheduleAuto;
+    hipSetDevice(0);
+    const hipError_t fe = hipSetDeviceFlags(flags);
+    if (fe != hipSuccess) BEE_WARN("hipSetDeviceFlags(%u): %s", flags, hipGetErrorString(fe));
+  }
   if (g_bk.init(0) != 0) {
     *err = std::string("bk_init: ") + g_bk.last_error();
     return false;

@@ -48,6 +48,34 @@ __global__ __launch_bounds__(256) void philox_uniform_f32(float* __restrict__ ou
   }
 }
 
+// bf16: the f32 stream's values rounded once to bf16 (RNE) -- bit-identical to
+// drawing f32 and casting, without the f32 buffer and the cast pass.  Each
+// lane handles two counters (8 values) for one 16-B store.
+__global__ __launch_bounds__(256) void philox_uniform_bf16(uint16_t* __restrict__ out, int64_t n, uint32_t k0,
+                                                           uint32_t k1, uint64_t offset, float lo, float span) {
+  const int64_t octs = (n + 7) / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < octs; o += stride) {
+    uint16_t h[8];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const uint64_t ctr = offset + 2 * (uint64_t)o + half;
+      const uint4 r = Philox::run(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), kTagUniformF32, 0u), k0, k1);
+      h[4 * half + 0] = float_to_bf16_bits(lo + span * u24(r.x));
+      h[4 * half + 1] = float_to_bf16_bits(lo + span * u24(r.y));
+      h[4 * half + 2] = float_to_bf16_bits(lo + span * u24(r.z));
+      h[4 * half + 3] = float_to_bf16_bits(lo + span * u24(r.w));
+    }
+    const int64_t i = 8 * o;
+    if (i + 7 < n) {
+      *reinterpret_cast<uint4*>(out + i) = make_uint4(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16),
+                                                      h[4] | ((uint32_t)h[5] << 16), h[6] | ((uint32_t)h[7] << 16));
+    } else {
+      for (int j = 0; i + j < n; ++j) out[i + j] = h[j];
+    }
+  }
+}
+
 // Standard normal via Box-Muller on the f32 / f64 streams (for randn).
 __global__ __launch_bounds__(256) void philox_normal_f32(float* __restrict__ out, int64_t n, uint32_t k0, uint32_t k1,
                                                          uint64_t offset, float mean, float std) {
@@ -95,7 +123,7 @@ __global__ __launch_bounds__(256) void philox_normal_f64(double* __restrict__ ou
 
 using namespace bk;
 
-// dtype: kF64 or kF32.  `offset` advances the counter so successive draws from
+// dtype: kF64, kF32 or kBF16 (the f32 stream, rounded).  `offset` advances the counter so successive draws from
 // one seed never overlap (the Python side keeps the running offset).
 BK_API int bk_rand_uniform(void* out, int64_t n, int dtype, uint64_t seed, uint64_t offset, double lo, double hi,
                            hipStream_t stream) {
@@ -105,6 +133,10 @@ BK_API int bk_rand_uniform(void* out, int64_t n, int dtype, uint64_t seed, uint6
   if (dtype == kF64) {
     const int64_t pairs = (n + 1) / 2;
     philox_uniform_f64<<<stream_grid(pairs, 256), 256, 0, stream>>>((double*)out, n, k0, k1, offset, lo, hi - lo);
+  } else if (dtype == kBF16) {
+    const int64_t octs = (n + 7) / 8;
+    philox_uniform_bf16<<<stream_grid(octs, 256), 256, 0, stream>>>((uint16_t*)out, n, k0, k1, offset, (float)lo,
+                                                                     (float)(hi - lo));
   } else if (dtype == kF32) {
     const int64_t quads = (n + 3) / 4;
     philox_uniform_f32<<<stream_grid(quads, 256), 256, 0, stream>>>((float*)out, n, k0, k1, offset, (float)lo,
