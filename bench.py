@@ -252,7 +252,14 @@ def executor_stats(hport):
         with urllib.request.urlopen(f"http://127.0.0.1:{hport}/v1/status", timeout=10) as f:
             st = json.load(f)
         keys = ("mean_warm_ms", "mean_worker_warm_ms", "mean_fork_ms", "mean_acquire_ms", "executions")
-        return [{k: round(s["executor"].get(k, 0), 3) for k in keys} for s in st["slots"]]
+        out = []
+        for s in st["slots"]:
+            e = s["executor"]
+            d = {k: round(e.get(k, 0), 3) for k in keys}
+            n = max(e.get("executions", 0), 1)
+            d["daemon_cpu_ms_per_exec"] = {k: round(v / n, 3) for k, v in (e.get("cpu_ms") or {}).items()}
+            out.append(d)
+        return out
     except Exception as e:  # noqa: BLE001
         return repr(e)[:200]
 

@@ -296,6 +296,7 @@ void KernelBroker::serve(int fd, pid_t peer) {
     if (len > kMaxFrame) break;
     payload.resize(len);
     if (len && !read_exact(fd, payload.data(), len)) break;
+    CpuScope cpu(kCpuBroker);
     Reader r{payload.data(), payload.size()};
     out.clear();
     int32_t st = kOk;

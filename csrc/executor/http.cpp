@@ -334,6 +334,7 @@ void HttpServer::handle_conn(int fd) {
                                              : lower(req.header("connection")) == "keep-alive";
 
     HttpResponse resp;
+    CpuScope cpu(kCpuHttp);
     try {
       handler_(req, resp);
     } catch (const std::exception& e) {

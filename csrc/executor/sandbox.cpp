@@ -251,6 +251,7 @@ void SandboxPool::zygote_reader(Zygote* z) {
   std::string buf, line;
   const int fd = z->fd;
   while (read_line(fd, buf, &line)) {
+    CpuScope cpu(kCpuZygoteIo);
     Json m;
     try {
       m = Json::parse(line);
@@ -498,6 +499,7 @@ void SandboxPool::worker_reader(int fd) {
   std::string buf, line;
   std::shared_ptr<Worker> w;
   while (read_line(fd, buf, &line)) {
+    CpuScope cpu(kCpuWorkerIo);
     Json m;
     try {
       m = Json::parse(line);
@@ -617,6 +619,7 @@ void SandboxPool::cleanup_loop() {
         // final sweep
       }
     }
+    CpuScope cpu(kCpuCleanup);
     std::deque<std::string> todo;
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -994,6 +997,9 @@ Json SandboxPool::status() {
   j.set("target", cfg_.target);
   j.set("light_target", target_of(kLight));
   j.set("min_target", target_of(kMin));
+  Json cpu = Json::object();
+  for (int i = 0; i < kCpuParts; ++i) cpu.set(kCpuPartNames[i], g_cpu_ns[i].load() / 1e6);
+  j.set("cpu_ms", cpu);
   j.set("ready", (int64_t)(ready_[kDirect].size() + ready_[kLight].size() + ready_[kMin].size()));
   j.set("ready_min", (int64_t)ready_[kMin].size());
   j.set("ready_direct", (int64_t)ready_[kDirect].size());
@@ -1042,6 +1048,10 @@ std::string SandboxPool::metrics_text() {
   line("bee_executor_workers_spawned_total", "counter", (double)m_spawned_.load());
   line("bee_executor_worker_spawn_failures_total", "counter", (double)m_spawn_failed_.load());
   line("bee_executor_idle_recycled_total", "counter", (double)m_recycled_.load());
+  s += "# TYPE bee_executor_cpu_seconds_total counter\n";
+  for (int i = 0; i < kCpuParts; ++i)
+    s += std::string("bee_executor_cpu_seconds_total{gpus=\"") + cfg_.gpus + "\",part=\"" + kCpuPartNames[i] + "\"} " +
+         std::to_string(g_cpu_ns[i].load() / 1e9) + "\n";
   line("bee_executor_inflight", "gauge", (double)m_inflight_.load());
   line("bee_executor_ready_workers", "gauge",
        (double)(ready_[kDirect].size() + ready_[kLight].size() + ready_[kMin].size()));

@@ -17,6 +17,9 @@
 
 namespace bee {
 
+std::atomic<int64_t> g_cpu_ns[kCpuParts];
+const char* const kCpuPartNames[kCpuParts] = {"http", "worker_io", "zygote_io", "broker", "cleanup"};
+
 static std::mutex g_log_mu;
 
 void log_line(const char* level, const char* fmt, ...) {

@@ -2,6 +2,9 @@
 #pragma once
 #include <sys/types.h>
 
+#include <time.h>
+
+#include <atomic>
 #include <cstdint>
 #include <map>
 #include <string>
@@ -18,6 +21,24 @@ void log_line(const char* level, const char* fmt, ...) __attribute__((format(pri
 // ---- time -----------------------------------------------------------------
 int64_t wall_ns();     // CLOCK_REALTIME
 double mono_ms();      // CLOCK_MONOTONIC, milliseconds
+
+// ---- CPU accounting ---------------------------------------------------------
+// Thread CPU time spent per daemon role, exported on /metrics and /v1/status
+// (which part of the per-request CPU budget the daemon itself costs).
+enum CpuPart { kCpuHttp = 0, kCpuWorkerIo, kCpuZygoteIo, kCpuBroker, kCpuCleanup, kCpuParts };
+extern std::atomic<int64_t> g_cpu_ns[kCpuParts];
+extern const char* const kCpuPartNames[kCpuParts];
+inline int64_t thread_cpu_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
+}
+struct CpuScope {
+  CpuPart part;
+  int64_t t0;
+  explicit CpuScope(CpuPart p) : part(p), t0(thread_cpu_ns()) {}
+  ~CpuScope() { g_cpu_ns[part] += thread_cpu_ns() - t0; }
+};
 
 // ---- ids ------------------------------------------------------------------
 std::string random_hex(size_t nbytes);  // getrandom(2)-backed
