@@ -231,6 +231,12 @@ def _finish(code: int, timing_path: Optional[str] = None, sock: Optional[socket.
         except Exception:
             pass
     _STAMPS["exit"] = time.monotonic() * 1e3
+    try:
+        ru = resource.getrusage(resource.RUSAGE_SELF)
+        _STAMPS["cpu_ms"] = (ru.ru_utime + ru.ru_stime) * 1e3
+        _STAMPS["minflt"] = ru.ru_minflt
+    except Exception:
+        pass
     status = code & 0xFF if code >= 0 else 1
     if timing_path:
         try:  # CLOCK_MONOTONIC ms, the executor's clock too

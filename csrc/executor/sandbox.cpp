@@ -956,6 +956,9 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
         timings.set("w_atexit", ex - s1);
         timings.set("w_reap", lead->t_exit - ex);
       }
+      // the sandbox process's own CPU (fork to exit, before teardown)
+      if (st["cpu_ms"].is_number()) timings.set("w_cpu", st["cpu_ms"].as_number());
+      if (st["minflt"].is_number()) timings.set("w_minflt", st["minflt"].as_number());
     } catch (...) {
     }
   }
