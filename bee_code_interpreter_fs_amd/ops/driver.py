@@ -157,6 +157,7 @@ def _info_dict(v, arch: str) -> dict:
 (HELLO, ALLOC, FREE, WRITE, READ, RAND, UNARY, BINARY, CAST, FILL, REDUCE, GEMM, TRANSPOSE, SYNC, MEMSTATS, INFO,
  COPY, RAND_REDUCE) = range(1, 19)
 _HDR = struct.Struct("<IIQ")
+_NO_REPLY = 1  # request flag: no response unless a later request collects an error
 _RHDR = struct.Struct("<iIQ")
 _CHUNK = 64 << 20
 
@@ -219,13 +220,20 @@ class BrokerDriver:
             raise BeekernError(text)
         return bytes(body)
 
+    def _post(self, op: int, payload: bytes) -> None:
+        """Fire-and-forget request (kernel launches, frees): no reply; a
+        failure is raised by the next request that waits for one (sync,
+        reduce, read, alloc) -- the asynchronous-error model of GPU streams."""
+        with self.lock:
+            self.sock.sendall(_HDR.pack(op, _NO_REPLY, len(payload)) + payload)
+
     def malloc(self, nbytes: int) -> int:
         return struct.unpack("<Q", self._call(ALLOC, struct.pack("<Q", max(int(nbytes), 1))))[0]
 
     def free(self, h: int) -> None:
         try:
-            self._call(FREE, struct.pack("<Q", h))
-        except (OSError, BeekernError):
+            self._post(FREE, struct.pack("<Q", h))
+        except OSError:
             pass
 
     def h2d(self, h: int, host: np.ndarray, offset: int = 0) -> None:
@@ -241,19 +249,19 @@ class BrokerDriver:
             self._call(READ, struct.pack("<QQQ", h, offset + i, len(piece)), out=piece)
 
     def rand(self, kind, h, n, dt, seed, off, a, b) -> None:
-        self._call(RAND, struct.pack("<IIQqQQdd", kind, dt, h, n, seed & 0xFFFFFFFFFFFFFFFF, off, a, b))
+        self._post(RAND, struct.pack("<IIQqQQdd", kind, dt, h, n, seed & 0xFFFFFFFFFFFFFFFF, off, a, b))
 
     def unary(self, op, dt, x, y, n) -> None:
-        self._call(UNARY, struct.pack("<IIQQq", op, dt, x, y, n))
+        self._post(UNARY, struct.pack("<IIQQq", op, dt, x, y, n))
 
     def binary(self, op, dt, mode, a, b, sc, y, n) -> None:
-        self._call(BINARY, struct.pack("<IIIIQQdQq", op, dt, mode, 0, a, b or 0, sc, y, n))
+        self._post(BINARY, struct.pack("<IIIIQQdQq", op, dt, mode, 0, a, b or 0, sc, y, n))
 
     def cast(self, s, d, x, y, n) -> None:
-        self._call(CAST, struct.pack("<IIQQq", s, d, x, y, n))
+        self._post(CAST, struct.pack("<IIQQq", s, d, x, y, n))
 
     def fill(self, y, nbytes, pattern, width) -> None:
-        self._call(FILL, struct.pack("<QqQII", y, nbytes, pattern, width, 0))
+        self._post(FILL, struct.pack("<QqQII", y, nbytes, pattern, width, 0))
 
     def reduce(self, op, dt, a, b, n) -> float:
         return struct.unpack("<d", self._call(REDUCE, struct.pack("<IIQQq", op, dt, a, b or 0, n)))[0]
@@ -263,13 +271,13 @@ class BrokerDriver:
         return struct.unpack("<d", self._call(RAND_REDUCE, payload))[0]
 
     def gemm(self, A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt) -> None:
-        self._call(GEMM, struct.pack("<QQQiiiiiiffii", A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, 0))
+        self._post(GEMM, struct.pack("<QQQiiiiiiffii", A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, 0))
 
     def transpose(self, src, dst, rows, cols, ldi, ldo) -> None:
-        self._call(TRANSPOSE, struct.pack("<QQiiii", src, dst, rows, cols, ldi, ldo))
+        self._post(TRANSPOSE, struct.pack("<QQiiii", src, dst, rows, cols, ldi, ldo))
 
     def copy(self, dst, src, nbytes) -> None:
-        self._call(COPY, struct.pack("<QQQQQ", dst, 0, src, 0, nbytes))
+        self._post(COPY, struct.pack("<QQQQQ", dst, 0, src, 0, nbytes))
 
     def sync(self) -> None:
         self._call(SYNC, b"")

@@ -30,6 +30,7 @@ enum Status : int32_t {
   kBadHandle = 6, kProtocol = 7,
 };
 constexpr uint64_t kMaxFrame = 1ull << 30;
+constexpr uint32_t kNoReply = 1;  // request flag
 
 int dsize(int dt) {
   switch (dt) {
@@ -264,6 +265,11 @@ void KernelBroker::serve(int fd, pid_t peer) {
   g_bk.malloc_(&scalar, 256);
   std::vector<char> payload;
   std::vector<char> out;
+  // fire-and-forget requests (flag kNoReply: launches, frees) send nothing;
+  // their first failure is returned by the next request that wants a reply
+  int32_t deferred_st = kOk;
+  std::vector<char> deferred_msg;
+  bool op_skip = false;
 
   auto lookup = [&](uint64_t h, uint64_t need, Buf** b) -> bool {
     auto it = bufs.find(h);
@@ -291,6 +297,7 @@ void KernelBroker::serve(int fd, pid_t peer) {
     uint32_t hdr[4];
     if (!read_exact(fd, hdr, sizeof hdr)) break;
     const uint32_t op = hdr[0];
+    const bool no_reply = (hdr[1] & kNoReply) != 0;
     uint64_t len;
     memcpy(&len, &hdr[2], 8);
     if (len > kMaxFrame) break;
@@ -301,12 +308,23 @@ void KernelBroker::serve(int fd, pid_t peer) {
     out.clear();
     int32_t st = kOk;
     ops_++;
+    if (!no_reply && deferred_st != kOk) {
+      // an earlier fire-and-forget op failed: report it at this sync point
+      // (CUDA-style asynchronous error), without running this request
+      st = deferred_st;
+      out = deferred_msg;
+      deferred_st = kOk;
+      deferred_msg.clear();
+      op_skip = true;
+    }
     auto put = [&](const void* p, size_t n) { out.insert(out.end(), (const char*)p, (const char*)p + n); };
     auto launched = [&](int rc) {
       if (rc != 0) st = rc;
     };
 
-    switch (op) {
+    switch (op_skip ? 0u : op) {
+      case 0:
+        break;
       case kHello: {
         int64_t q = quota_fn_(peer);
         put(&q, 8);
@@ -534,9 +552,19 @@ void KernelBroker::serve(int fd, pid_t peer) {
       default:
         st = kProtocol;
     }
-    if (st == kLaunchFailed || st == kBadArgument) {
+    if (!op_skip && (st == kLaunchFailed || st == kBadArgument)) {
       const char* e = g_bk.last_error ? g_bk.last_error() : "";
       out.assign(e, e + strlen(e));
+    }
+    op_skip = false;
+    if (no_reply) {
+      if (st != kOk && deferred_st == kOk) {
+        deferred_st = st;
+        const std::string what = "deferred from op " + std::to_string(op) + (out.empty() ? "" : ": ");
+        deferred_msg.assign(what.begin(), what.end());
+        deferred_msg.insert(deferred_msg.end(), out.begin(), out.end());
+      }
+      continue;
     }
     uint32_t rh[4];
     int32_t s32 = st;

@@ -57,17 +57,20 @@ def test_broker_rejects_out_of_bounds(gsvc):
         "x = bk.empty((16,), 'float64')\n"
         "try:\n"
         "    driver().unary(0, 1, x.ptr, x.ptr, 1 << 30)\n"
+        "    driver().sync()  # launches are asynchronous: errors surface at the next sync\n"
         "    print('unchecked')\n"
         "except bk.BeekernError as e:\n"
         "    print('rejected')\n"
         "try:\n"
         "    driver().unary(0, 1, 987654, x.ptr, 4)\n"
+        "    driver().sync()\n"
         "    print('unchecked')\n"
         "except bk.BeekernError as e:\n"
         "    print('rejected')\n"
+        "print(float(bk.sum(x)))  # the session stays usable after an error\n"
     )
     r = run(gsvc, code)
-    assert r.stdout.split() == ["rejected", "rejected"], (r.stdout, r.stderr)
+    assert r.stdout.split() == ["rejected", "rejected", "0.0"], (r.stdout, r.stderr)
 
 
 def test_torch_inside_sandbox(gsvc):
