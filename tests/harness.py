@@ -113,3 +113,53 @@ def wait_for(pred, timeout=30.0, interval=0.05):
             return True
         time.sleep(interval)
     return False
+
+
+COWSAY_MODULE = '''"""Offline stand-in for the ``cowsay`` distribution (test wheelhouse)."""
+
+
+def cow(text):
+    line = "_" * (len(text) + 2)
+    print(" " + line)
+    print("| " + text + " |")
+    print(" " + "=" * (len(text) + 2))
+    print("        \\\\   ^__^")
+    print("         \\\\  (oo)\\\\_______")
+    print("            (__)\\\\       )\\\\/\\\\")
+    print("                ||----w |")
+    print("                ||     ||")
+'''
+
+
+def build_test_wheelhouse(directory: str) -> str:
+    """Write a pure-Python ``cowsay`` wheel into ``directory``.
+
+    The reference's ``test_ad_hoc_import`` (`test/e2e/test_grpc.py:70-75`)
+    needs ``pip install cowsay`` from PyPI; these machines have no package
+    index, so the test installs this wheel through the same offline path a
+    deployment uses (``APP_WHEELHOUSE``)."""
+    import base64
+    import hashlib
+    import zipfile
+
+    os.makedirs(directory, exist_ok=True)
+    name, version = "cowsay", "6.1"
+    dist = f"{name}-{version}.dist-info"
+    files = {
+        f"{name}/__init__.py": COWSAY_MODULE,
+        f"{dist}/METADATA": f"Metadata-Version: 2.1\nName: {name}\nVersion: {version}\nSummary: test stand-in\n",
+        f"{dist}/WHEEL": "Wheel-Version: 1.0\nGenerator: bee-tests\nRoot-Is-Purelib: true\nTag: py3-none-any\n",
+        f"{dist}/top_level.txt": f"{name}\n",
+    }
+    record = []
+    for path, text in files.items():
+        data = text.encode()
+        digest = base64.urlsafe_b64encode(hashlib.sha256(data).digest()).rstrip(b"=").decode()
+        record.append(f"{path},sha256={digest},{len(data)}")
+    record.append(f"{dist}/RECORD,,")
+    files[f"{dist}/RECORD"] = "\n".join(record) + "\n"
+    wheel = os.path.join(directory, f"{name}-{version}-py3-none-any.whl")
+    with zipfile.ZipFile(wheel, "w", zipfile.ZIP_DEFLATED) as z:
+        for path, text in files.items():
+            z.writestr(path, text)
+    return directory

@@ -4,8 +4,10 @@
 Mirrors the reference's black-box suites (`test/e2e/test_grpc.py`,
 `test/e2e/test_http.py`) case by case, for both APIs.
 ``test_ad_hoc_import`` needs ``pip install cowsay`` from a package index,
-which does not exist on these machines; it runs against a local wheelhouse
-when ``BEE_TEST_WHEELHOUSE`` points at one and is skipped otherwise.
+which does not exist on these machines; the service here is configured with
+a local wheelhouse holding a pure-Python ``cowsay`` wheel built by the
+fixture (``harness.build_test_wheelhouse``), so the sandbox's import scan +
+offline install path runs for real.
 """
 
 import json
@@ -18,7 +20,7 @@ import pytest
 
 from bee_code_interpreter_fs_amd.models import proto as pb
 
-from .harness import ServiceHarness, ensure_native_executor
+from .harness import ServiceHarness, build_test_wheelhouse, ensure_native_executor
 
 USING_IMPORTS = textwrap.dedent(
     """
@@ -111,7 +113,8 @@ BAD_TOOL_ERRORS = {
 @pytest.fixture(scope="module")
 def service(tmp_path_factory):
     ensure_native_executor()
-    h = ServiceHarness(str(tmp_path_factory.mktemp("svc")), default_timeout=30.0)
+    wheelhouse = build_test_wheelhouse(str(tmp_path_factory.mktemp("wheelhouse")))
+    h = ServiceHarness(str(tmp_path_factory.mktemp("svc")), default_timeout=30.0, wheelhouse=wheelhouse)
     h.start()
     yield h
     h.stop()
@@ -379,7 +382,17 @@ def test_sandbox_patches_produce_files(http):
     assert r["stdout"].strip().endswith("date")
 
 
-@pytest.mark.skipif(not os.environ.get("BEE_TEST_WHEELHOUSE"), reason="needs a local wheelhouse with cowsay (no package index)")
 def test_ad_hoc_import(http):
+    """`test/e2e/test_http.py:34-44`: a missing import is installed before the run."""
     r = http.post("/v1/execute", json={"source_code": "import cowsay\ncowsay.cow('Hello World')", "files": {}})
+    assert r.json()["exit_code"] == 0, r.json()["stderr"]
     assert "Hello World" in r.json()["stdout"]
+
+
+def test_grpc_ad_hoc_import(stub):
+    """`test/e2e/test_grpc.py:70-75`, and the install stays in that sandbox."""
+    r = stub.Execute(pb.ExecuteRequest(source_code="import cowsay\ncowsay.cow('Hello World')"))
+    assert r.exit_code == 0, r.stderr
+    assert "Hello World" in r.stdout
+    r = stub.Execute(pb.ExecuteRequest(source_code="import importlib.util\nprint(importlib.util.find_spec('cowsay') is None)"))
+    assert r.stdout == "True\n"
