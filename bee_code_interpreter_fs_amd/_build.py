@@ -63,7 +63,7 @@ def _targets() -> List[Target]:
             compiler=HIPCC,
             compile_flags=HIP_FLAGS,
             link_flags=[f"--offload-arch={ARCH}", "-shared", "-fPIC"],
-            headers=[os.path.join(k, "bk_common.hpp"), os.path.join(k, "bk_philox.hpp")],
+            headers=[os.path.join(k, "bk_common.hpp"), os.path.join(k, "bk_philox.hpp"), os.path.join(k, "gemm256_impl.hpp")],
             hip=True,
         ),
     ]
@@ -125,6 +125,21 @@ def _targets() -> List[Target]:
                 compiler=CXX,
                 compile_flags=["-O2", "-fPIC", "-std=c++17", "-Wall", "-U_FORTIFY_SOURCE", "-fvisibility=default"],
                 link_flags=["-shared", "-fPIC", "-ldl"],
+            )
+        )
+    lab = os.path.join(ROOT, "tools", "gemm_lab")
+    if os.path.isdir(lab):
+        targets.append(
+            Target(
+                name="gemm-lab",
+                output=os.path.join(lab, "libgemmlab.so"),
+                sources=[os.path.join(lab, "gemm_lab.hip")],
+                compiler=HIPCC,
+                compile_flags=HIP_FLAGS,
+                link_flags=[f"--offload-arch={ARCH}", "-shared", "-fPIC"],
+                headers=[os.path.join(k, "bk_common.hpp"), os.path.join(k, "gemm256_impl.hpp")],
+                hip=True,
+                optional=True,
             )
         )
     if os.path.isdir(rb) and os.listdir(rb):

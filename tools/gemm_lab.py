@@ -1,0 +1,119 @@
+"""A/B of the 256x256 bf16 GEMM schedule variants (tools/gemm_lab/gemm_lab.hip)
+in ONE process, interleaved (guide §5.4 rules 19/24), against hipBLASLt on the
+same uniform [-1, 1) operands (rule 25).
+
+Per variant: max |err| vs an fp32 torch reference and a race screen
+(bitwise-identical repeats -- the kernels are deterministic, so any
+difference is a race) on shapes that hit the 1-, 2- and 3-K-tile edge paths;
+diagnostic variants (L2-resident operands) are timed only.
+
+    python -m bee_code_interpreter_fs_amd._build gemm-lab   # on the CPU box
+    python tools/gemm_lab.py [--rounds 7] [--reps 20]
+"""
+
+import argparse
+import ctypes
+import json
+import os
+import statistics
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NAMES = {0: "round1", 1: "keep_b0", 2: "round1_nostagger", 3: "keep_b0_nostagger", 4: "diag_round1_l2", 5: "diag_keep_b0_l2"}
+DIAG = {4, 5}
+
+
+def load():
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "gemm_lab", "libgemmlab.so"))
+    lib.gemmlab_run.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 7 + [ctypes.c_void_p]
+    lib.gemmlab_run.restype = ctypes.c_int
+    return lib
+
+
+def run(lib, v, a, bt, c):
+    M, K = a.shape
+    N = bt.shape[0]
+    rc = lib.gemmlab_run(v, a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, N, int(c.dtype == torch.bfloat16),
+                         torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"variant {v} rc={rc} {M}x{N}x{K}")
+
+
+def check(lib, variants, M, N, K, repeats):
+    g = torch.Generator(device="cuda").manual_seed(M * 131 + N * 7 + K)
+    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    bt = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    ref = a.float() @ bt.float().T
+    out = {}
+    for v in variants:
+        c = torch.full((M, N), float("nan"), device="cuda", dtype=torch.float32)
+        run(lib, v, a, bt, c)
+        torch.cuda.synchronize()
+        err = (c - ref).abs().max().item()
+        first = c.clone()
+        mism = 0
+        for _ in range(repeats):
+            c.fill_(float("nan"))
+            run(lib, v, a, bt, c)
+            mism += int(not torch.equal(c, first))
+        torch.cuda.synchronize()
+        out[NAMES[v]] = {"max_abs_err": err, "racy_repeats": mism, "ok": bool(err < 1e-3 * K ** 0.5 and mism == 0)}
+    return out
+
+
+def bench(lib, variants, M, N, K, rounds, reps):
+    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
+    bt = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
+    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    fns = {NAMES[v]: (lambda v=v: run(lib, v, a, bt, c)) for v in variants}
+    fns["hipblaslt"] = lambda: torch.matmul(a, bt.T, out=c)
+    for f in fns.values():
+        for _ in range(5):
+            f()
+    times = {k: [] for k in fns}
+    for _ in range(rounds):
+        for name, f in fns.items():
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                f()
+            e.record()
+            e.synchronize()
+            times[name].append(s.elapsed_time(e) / reps)
+    flops = 2.0 * M * N * K
+    return {name: {"us_median": round(1e3 * statistics.median(t), 2), "us_min": round(1e3 * min(t), 2),
+                   "TFLOPs_median": round(flops / statistics.median(t) / 1e9, 1)} for name, t in times.items()}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rounds", type=int, default=7)
+    p.add_argument("--reps", type=int, default=20)
+    p.add_argument("--repeats", type=int, default=8)
+    p.add_argument("--variants", type=int, nargs="*", default=None)
+    p.add_argument("--no-check", action="store_true")
+    p.add_argument("--one", type=int, default=None, help="only run this variant (-1 = hipBLASLt) --reps times at 4096^3 (rocprofv3 passes)")
+    args = p.parse_args()
+    torch.cuda.init()
+    lib = load()
+    if args.one is not None:
+        a = torch.empty(4096, 4096, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
+        bt = torch.empty(4096, 4096, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
+        c = torch.empty(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        for _ in range(args.reps):
+            run(lib, args.one, a, bt, c) if args.one >= 0 else torch.matmul(a, bt.T, out=c)
+        torch.cuda.synchronize()
+        return
+    variants = args.variants if args.variants is not None else list(range(lib.gemmlab_count()))
+    real = [v for v in variants if v not in DIAG]
+    if not args.no_check:
+        for M, N, K in [(256, 256, 64), (256, 512, 128), (512, 256, 192), (512, 512, 256), (2048, 2048, 320),
+                        (4096, 4096, 4096), (1280, 3840, 1088), (8192, 4096, 1024)]:
+            print(json.dumps({"check": f"{M}x{N}x{K}", **check(lib, real, M, N, K, args.repeats)}), flush=True)
+    for M, N, K in [(4096, 4096, 4096), (8192, 8192, 8192), (4096, 4096, 64), (4096, 4096, 1024)]:
+        print(json.dumps({"bench": f"{M}x{N}x{K}", **bench(lib, variants, M, N, K, args.rounds, args.reps)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

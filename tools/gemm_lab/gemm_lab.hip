@@ -1,0 +1,40 @@
+// GEMM schedule lab: every 256x256 schedule variant in ONE binary, so
+// tools/gemm_lab.py can A/B them interleaved in one process (guide §5.4
+// rules 19/24).  Not part of libbeekern.
+#include "../../csrc/kernels/gemm256_impl.hpp"
+
+using namespace bk;
+
+namespace {
+constexpr int kLabOpts[] = {
+    g256::kOptRound1,           // 0: round-1 schedule (shipped until a variant wins)
+    g256::kOptKeepB0,           // 1: B0 kept in registers, every half >= 5 phases ahead
+    0,                          // 2: round-1 without the wave-group stagger
+    g256::kKeepB0,              // 3: keep-B0 without the stagger
+    g256::kStagger | g256::kSameTile,  // 4: DIAGNOSTIC round-1 on L2-resident operands (wrong C)
+    g256::kOptKeepB0 | g256::kSameTile,  // 5: DIAGNOSTIC keep-B0 on L2-resident operands (wrong C)
+};
+template <int I>
+void run(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool bf,
+         hipStream_t s) {
+  g256::launch<kLabOpts[I]>(A, B, C, M, N, K, lda, ldb, ldc, 1.0f, 0.0f, bf, s);
+}
+}  // namespace
+
+BK_API int gemmlab_count() { return (int)(sizeof(kLabOpts) / sizeof(kLabOpts[0])); }
+
+BK_API int gemmlab_run(int variant, const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb,
+                       int ldc, int out_bf16, hipStream_t s) {
+  if (!g256::ok(M, N, K, lda, ldb, ldc, out_bf16 != 0)) return kBadArgument;
+  const bool bf = out_bf16 != 0;
+  switch (variant) {
+    case 0: run<0>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 1: run<1>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 2: run<2>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 3: run<3>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 4: run<4>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 5: run<5>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    default: return kBadArgument;
+  }
+  return launch_status();
+}
