@@ -137,7 +137,7 @@ def _targets() -> List[Target]:
                 compiler=HIPCC,
                 compile_flags=HIP_FLAGS,
                 link_flags=[f"--offload-arch={ARCH}", "-shared", "-fPIC"],
-                headers=[os.path.join(k, "bk_common.hpp"), os.path.join(k, "gemm256_impl.hpp")],
+                headers=[os.path.join(k, "bk_common.hpp"), os.path.join(k, "gemm256_impl.hpp"), os.path.join(k, "gemm256w4_impl.hpp")],
                 hip=True,
                 optional=True,
             )

@@ -1,0 +1,299 @@
+// bf16 GEMM, 256x256 block tile, FOUR waves of 128x128: C = alpha * A . Bt^T (+ beta C)
+//
+// Why four waves (measured, profiles/r1_gemm_lab.log + PMC): the 8-wave
+// 128x64-per-wave kernel (gemm256_impl.hpp) issues 238 ds_read_b128 per CU
+// per K-tile and runs 8 barriers per K-tile; its MFMA pipes were busy 58% of
+// the cycles, and moving its operands into L2 (diagnostic variant) bought only
+// 2%, so the limiter is inside the CU, not HBM.  A 128x128 wave tile reads
+// each A row and B column once per 128 outputs instead of per 64: 128
+// ds_read_b128 per CU per K-tile (32 per wave), and the whole K-tile needs ONE
+// barrier.
+//
+// Geometry: 256 threads = 4 waves as 2 (M) x 2 (N), one wave per SIMD; each
+// wave owns 8x8 fragments of v_mfma_f32_16x16x32_bf16 = 256 accumulator
+// registers (the unified VGPR/AGPR file gives one wave 512).  BK = 64.
+//
+// LDS (one __shared__ array, 128 KiB): two K-tile buffers of [A 256x64 | B
+// 256x64] bf16, rows of 128 B with the 16-B chunk XOR swizzle of
+// gemm256_impl.hpp (chunk c of row r at c ^ ((r >> 1) & 7): conflict-free
+// ds_read_b128), staged by buffer_load ... lds (16 per wave per K-tile)
+// through one buffer descriptor per operand panel.
+//
+// Loop (K-tile t in buffer cur = t & 1, fragments double-buffered in
+// registers by k-half s):
+//     ds_read  frags(t, s=1)                      [cur]
+//     64 MFMA  frags(t, s=0)
+//     s_waitcnt lgkmcnt(0) vmcnt(0)               own reads of cur done; own
+//     s_barrier                                   glds of t+1 landed
+//     glds     tile t+2 -> cur                    WAR-safe: every wave passed
+//     ds_read  frags(t+1, s=0)        [nxt]       RAW-safe: every wave's t+1
+//     64 MFMA  frags(t, s=1)                      loads retired pre-barrier
+// so the MFMA stream only stops at the barrier, every LDS read has 64 MFMAs
+// (>= 1024 cycles) to land, and every K-tile load has one whole iteration.
+// The only vmcnt(0) in the loop waits for loads issued an iteration earlier.
+#pragma once
+#include "bk_common.hpp"
+
+namespace bk {
+namespace g4 {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef const __attribute__((address_space(1))) void* global_void_ptr;
+
+constexpr int TM = 256, TN = 256, TK = 64;
+constexpr int kThreads = 256;
+constexpr int kOperand = 256 * TK;   // elements of one operand's K-tile (32 KiB)
+constexpr int kBuf = 2 * kOperand;   // A | B
+constexpr int kGroupM = 4;           // tiles along M sharing a B panel in L2
+constexpr int kGlds = kOperand / (kThreads * 8);  // glds per wave per operand per K-tile (8)
+// epilogue staging: per wave 32 rows x 128 f32, pitch 132 (4 rows of the
+// 16x16 C map land 16 banks apart: conflict-free ds_write_b32)
+constexpr int kEpPitch = 132;
+constexpr int kEpRows = 32;
+constexpr int kEpWaveFloats = kEpRows * kEpPitch;
+constexpr int kSmemBytes = 2 * kBuf * 2;  // 128 KiB (epilogue needs 66 KiB)
+static_assert(4 * kEpWaveFloats * 4 <= kSmemBytes, "epilogue staging fits");
+
+// options
+enum : int {
+  kPinOrder = 1,    // sched_barrier fences around each MFMA block
+  kInterleave = 2,  // sched_group_barrier: spread ds_read / glds among the MFMAs
+};
+
+__device__ __forceinline__ int xcd_remap(int b, int nblocks) {
+  const int xcd = b % kNumXCD, q = nblocks / kNumXCD, r = nblocks % kNumXCD;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + b / kNumXCD;
+}
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// One operand's 256-row panel as a buffer resource (SRD in SGPRs): loads
+// address it with a 2-VGPR per-lane offset + an SGPR offset instead of 16
+// 64-bit per-lane pointers, and rows past the panel read as zero.
+struct Panel {
+  __amdgpu_buffer_rsrc_t rsrc;
+  int lane_off[2];  // bytes: (lane/8) rows + this lane's swizzled 16-B chunk, for even / odd i
+  int row_bytes;    // ld * 2
+};
+
+__device__ __forceinline__ Panel make_panel(const uint16_t* base, int ld, int lane) {
+  Panel p;
+  // descriptor inputs readfirstlane'd so the compiler can PROVE the SRD
+  // uniform (else it wraps every load in a waterfall loop: guide T20)
+  const uint64_t addr = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)addr);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32));
+  const int64_t span = (int64_t)256 * ld * 2;  // integer clamp (HIP's min() has no int64 overload: it went through f64)
+  const uint32_t bytes = __builtin_amdgcn_readfirstlane(span > 0xffffffffll ? 0xffffffffu : (uint32_t)span);
+  p.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+  p.row_bytes = ld * 2;
+  // row r = wave*64 + i*8 + lane/8 -> swizzle key (r>>1)&7 = (i*4 + lane/16)&7
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int c = (lane & 7) ^ ((par * 4 + (lane >> 4)) & 7);
+    p.lane_off[par] = (lane >> 3) * ld * 2 + c * 16;
+  }
+  return p;
+}
+
+// stage one operand's K-tile: 8 wave-instructions of 1 KiB (8 rows) each;
+// `wave` must be wave-uniform (readfirstlane'd) so the LDS base goes to M0
+__device__ __forceinline__ void stage(const Panel& p, int k0, uint16_t* lds_operand, int wave) {
+#pragma unroll
+  for (int i = 0; i < kGlds; ++i) {
+    const int soff = (wave * 64 + i * 8) * p.row_bytes + k0 * 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(p.rsrc, (lds_void_ptr)(lds_operand + (wave * kGlds + i) * 8 * TK), 16,
+                                             p.lane_off[i & 1], soff, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 frag(const uint16_t* lds_operand, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(lds_operand + row * TK + swz(row, chunk) * 8);
+}
+
+// the 8 A (rows wr*128 + i*16 + lane&15) and 8 B fragments of k-half s
+__device__ __forceinline__ void read_frags(const uint16_t* buf, int wr, int wc, int lane, int s, bf16x8 (&fa)[8],
+                                           bf16x8 (&fb)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa[i] = frag(buf, wr * 128 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fb[j] = frag(buf + kOperand, wc * 128 + j * 16 + (lane & 15), s * 4 + (lane >> 4));
+}
+
+__device__ __forceinline__ void mfma_block(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+}
+
+// 64 MFMAs with `ds` ds_reads and `vm` VMEM ops spread evenly among them
+template <int DS, int VM>
+__device__ __forceinline__ void interleave_hint() {
+  constexpr int slots = 16;
+#pragma unroll
+  for (int q = 0; q < slots; ++q) {
+    if constexpr (VM > 0) __builtin_amdgcn_sched_group_barrier(0x020, VM / slots, 0);
+    if constexpr (DS > 0) __builtin_amdgcn_sched_group_barrier(0x100, DS / slots, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+  }
+}
+
+template <bool OUT_BF16>
+__device__ __forceinline__ void epilogue(uint16_t* smem, const f32x4 (&acc)[8][8], void* __restrict__ C, int ldc,
+                                         int64_t row0, int col0, int wave, int lane, float alpha, float beta) {
+  float* ep = reinterpret_cast<float*>(smem) + wave * kEpWaveFloats;
+#pragma unroll
+  for (int half = 0; half < 4; ++half) {  // 32 output rows (2 fragment rows) per round
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          ep[(ii * 16 + (lane >> 4) * 4 + r) * kEpPitch + j * 16 + (lane & 15)] = alpha * acc[half * 2 + ii][j][r];
+    const int64_t grow0 = row0 + half * 32;
+    if constexpr (OUT_BF16) {
+      // 16 lanes x 8 columns per row, 4 rows per pass
+#pragma unroll
+      for (int it = 0; it < kEpRows / 4; ++it) {
+        const int row = it * 4 + (lane >> 4), col = (lane & 15) * 8;
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(ep + row * kEpPitch + col);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(ep + row * kEpPitch + col + 4);
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        uint4* dst = reinterpret_cast<uint4*>((uint16_t*)C + (grow0 + row) * ldc + col0 + col);
+        if (beta != 0.f) {
+          const uint4 old = *dst;
+          const uint32_t w[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[2 * e] += beta * bf16_bits_to_float((uint16_t)(w[e] & 0xffff));
+            v[2 * e + 1] += beta * bf16_bits_to_float((uint16_t)(w[e] >> 16));
+          }
+        }
+        uint32_t packed[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          packed[e] = (uint32_t)float_to_bf16_bits(v[2 * e]) | ((uint32_t)float_to_bf16_bits(v[2 * e + 1]) << 16);
+        *dst = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+      }
+    } else {
+      // 32 lanes x 4 columns per row, 2 rows per pass
+#pragma unroll
+      for (int it = 0; it < kEpRows / 2; ++it) {
+        const int row = it * 2 + (lane >> 5), col = (lane & 31) * 4;
+        f32x4 v = *reinterpret_cast<const f32x4*>(ep + row * kEpPitch + col);
+        f32x4* dst = reinterpret_cast<f32x4*>((float*)C + (grow0 + row) * ldc + col0 + col);
+        if (beta != 0.f) v += beta * *dst;
+        *dst = v;
+      }
+    }
+  }
+}
+
+template <bool OUT_BF16, int O>
+__global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t* __restrict__ A,
+                                                                  const uint16_t* __restrict__ Bt,
+                                                                  void* __restrict__ C, int M, int N, int K, int lda,
+                                                                  int ldb, int ldc, float alpha, float beta) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[kSmemBytes / 2];  // the only LDS object
+  constexpr bool pin = (O & kPinOrder) != 0, inter = (O & kInterleave) != 0;
+
+  const int nbm = M / TM, nbn = N / TN, nblocks = nbm * nbn;
+  const int b = xcd_remap(blockIdx.x, nblocks);
+  const int group = kGroupM * nbn;
+  const int first_m = (b / group) * kGroupM;
+  const int gm = min(nbm - first_m, kGroupM);
+  const int tm = first_m + (b % group) % gm, tn = (b % group) / gm;
+  const int m0 = tm * TM, n0 = tn * TN;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const Panel pa = make_panel(A + (int64_t)m0 * lda, lda, lane);
+  const Panel pb = make_panel(Bt + (int64_t)n0 * ldb, ldb, lane);
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / TK;
+  // prologue: tiles 0 and 1 in flight, wait for tile 0 (16 glds per tile)
+  stage(pa, 0, smem, wave);
+  stage(pb, 0, smem + kOperand, wave);
+  if (nk > 1) {
+    stage(pa, TK, smem + kBuf, wave);
+    stage(pb, TK, smem + kBuf + kOperand, wave);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  barrier();
+
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  read_frags(smem, wr, wc, lane, 0, fa0, fb0);
+  for (int t = 0; t < nk; ++t) {
+    uint16_t* cur = smem + (t & 1) * kBuf;
+    uint16_t* nxt = smem + ((t & 1) ^ 1) * kBuf;
+
+    read_frags(cur, wr, wc, lane, 1, fa1, fb1);
+    if constexpr (inter) interleave_hint<16, 0>();
+    else if constexpr (pin) __builtin_amdgcn_sched_barrier(0);
+    mfma_block(acc, fa0, fb0);
+    if constexpr (pin || inter) __builtin_amdgcn_sched_barrier(0);
+
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    barrier();
+
+    // branch-free so the loads can be spread among the MFMAs below: past
+    // the end, re-stage the last K-tile into the buffer nobody reads again
+    // and read fragments nobody uses
+    const int kn = min(t + 2, nk - 1) * TK;
+    stage(pa, kn, cur, wave);
+    stage(pb, kn, cur + kOperand, wave);
+    read_frags(nxt, wr, wc, lane, 0, fa0, fb0);
+    if constexpr (inter) interleave_hint<16, 16>();
+    else if constexpr (pin) __builtin_amdgcn_sched_barrier(0);
+    mfma_block(acc, fa1, fb1);
+    if constexpr (pin || inter) __builtin_amdgcn_sched_barrier(0);
+  }
+
+  // every wave's last LDS reads and tail glds retired before any wave's
+  // staging writes
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  barrier();
+  epilogue<OUT_BF16>(smem, acc, C, ldc, m0 + wr * 128, n0 + wc * 128, wave, lane, alpha, beta);
+}
+
+inline bool ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16) {
+  return M > 0 && N > 0 && K > 0 && M % TM == 0 && N % TN == 0 && K % TK == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+         ldc % (out_bf16 ? 8 : 4) == 0;
+}
+
+template <int O>
+inline void launch(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
+                   float beta, bool out_bf16, hipStream_t stream) {
+  const unsigned grid = (unsigned)((M / TM) * (N / TN));
+  if (out_bf16)
+    gemm_bf16_tn_256w4<true, O><<<grid, kThreads, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N, K,
+                                                               lda, ldb, ldc, alpha, beta);
+  else
+    gemm_bf16_tn_256w4<false, O><<<grid, kThreads, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N, K,
+                                                                lda, ldb, ldc, alpha, beta);
+}
+
+}  // namespace g4
+}  // namespace bk

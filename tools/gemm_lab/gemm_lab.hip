@@ -2,6 +2,7 @@
 // tools/gemm_lab.py can A/B them interleaved in one process (guide §5.4
 // rules 19/24).  Not part of libbeekern.
 #include "../../csrc/kernels/gemm256_impl.hpp"
+#include "../../csrc/kernels/gemm256w4_impl.hpp"
 
 using namespace bk;
 
@@ -21,7 +22,15 @@ void run(const void* A, const void* B, void* C, int M, int N, int K, int lda, in
 }
 }  // namespace
 
-BK_API int gemmlab_count() { return (int)(sizeof(kLabOpts) / sizeof(kLabOpts[0])); }
+// 4-wave 128x128-per-wave kernel options, lab ids 6..
+constexpr int kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave};
+template <int I>
+void run_w4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool bf,
+            hipStream_t s) {
+  g4::launch<kW4Opts[I]>(A, B, C, M, N, K, lda, ldb, ldc, 1.0f, 0.0f, bf, s);
+}
+
+BK_API int gemmlab_count() { return (int)(sizeof(kLabOpts) / sizeof(kLabOpts[0]) + sizeof(kW4Opts) / sizeof(kW4Opts[0])); }
 
 BK_API int gemmlab_run(int variant, const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb,
                        int ldc, int out_bf16, hipStream_t s) {
@@ -34,6 +43,9 @@ BK_API int gemmlab_run(int variant, const void* A, const void* Bt, void* C, int 
     case 3: run<3>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 4: run<4>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 5: run<5>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 6: run_w4<0>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 7: run_w4<1>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 8: run_w4<2>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     default: return kBadArgument;
   }
   return launch_status();
