@@ -10,11 +10,16 @@ struct Philox {
   static constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
   static constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 
+  // Each round's 32x32->64 products as ONE v_mad_u64_u32 apiece instead of
+  // v_mul_hi_u32 + v_mul_lo_u32 (two quarter-rate ops): the generator is
+  // VALU-bound, and tools/probe/philox_probe.hip measured a 1e8-f64
+  // generate->square->sum loop 147 -> 120 us on MI355X.  Same bits.
   __device__ __forceinline__ static uint4 run(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-      const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
-      const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+      const uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
+      const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+      const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
       c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
       k0 += W0;
       k1 += W1;

@@ -34,6 +34,39 @@ def test_uniform_range_and_moments(gpu, dtype, n):
     np.testing.assert_array_equal(h, y)
 
 
+@pytest.mark.parametrize("n", [1, 7, 4099, 1 << 20])
+def test_uniform_streams_match_host_philox_bitwise(gpu, n):
+    """Every element of the f64 / f32 U[0,1) streams equals the host
+    Philox4x32-10 reference (tests/philox_ref.py, checked against the
+    Random123 known-answer vectors), including after an offset advance.
+    Scaled draws (lo + span*u) are one fused multiply-add on the GPU, so
+    they are held to 1 ulp of the unfused host expression."""
+    from .philox_ref import uniform_f32, uniform_f64
+
+    seed = 0x1234_5678_9ABC_DEF0
+    g = gpu.random.default_rng(seed)
+    np.testing.assert_array_equal(g.random(n).numpy(), uniform_f64(n, seed))
+    off = (n + 1) // 2  # the generator's counter advance for that draw
+    np.testing.assert_array_equal(g.random(n).numpy(), uniform_f64(n, seed, off))
+    np.testing.assert_array_equal(gpu.random.default_rng(seed).random(n, dtype="float32").numpy(), uniform_f32(n, seed))
+    np.testing.assert_array_max_ulp(gpu.random.default_rng(seed).uniform(-2.0, 3.0, n).numpy(),
+                                    uniform_f64(n, seed, 0, -2.0, 3.0), maxulp=1)
+    np.testing.assert_array_max_ulp(gpu.random.default_rng(seed).uniform(-1, 1, n, dtype="float32").numpy(),
+                                    uniform_f32(n, seed, 0, -1.0, 1.0), maxulp=1)
+
+
+def test_fused_rand_square_sum_matches_host_reference(gpu):
+    """The headline payload's lowering -- sum(square(rand(n))) as one fused
+    Philox->square->reduce kernel -- against an fp64 host sum of the
+    reference stream."""
+    from .philox_ref import uniform_f64
+
+    n = 3_000_001
+    got = float(gpu.sum(gpu.square(gpu.random.default_rng(99).random(n))))
+    ref = float(np.square(uniform_f64(n, 99)).sum())
+    assert abs(got - ref) <= 1e-9 * abs(ref)
+
+
 def test_uniform_offsets_do_not_overlap(gpu):
     g = gpu.random.default_rng(7)
     a = g.random(1000).numpy()
