@@ -293,6 +293,9 @@ def worker_main(spawn: dict) -> None:
         if job is None or job.get("op") != "run":
             os._exit(0)
         _STAMPS["recv"] = time.monotonic() * 1e3
+        ru = resource.getrusage(resource.RUSAGE_SELF)  # CPU spent while pooled (warm-up, prefault)
+        _STAMPS["cpu_pool_ms"] = (ru.ru_utime + ru.ru_stime) * 1e3
+        _STAMPS["minflt_pool"] = ru.ru_minflt
         for k, v in (job.get("env") or {}).items():
             os.environ[k] = str(v)
         quota = int(job.get("hbm_quota") or 0)

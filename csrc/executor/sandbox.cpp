@@ -959,6 +959,9 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
       // the sandbox process's own CPU (fork to exit, before teardown)
       if (st["cpu_ms"].is_number()) timings.set("w_cpu", st["cpu_ms"].as_number());
       if (st["minflt"].is_number()) timings.set("w_minflt", st["minflt"].as_number());
+      // of which spent while waiting in the pool (warm-up, prefault): off the request path
+      if (st["cpu_pool_ms"].is_number()) timings.set("w_cpu_pool", st["cpu_pool_ms"].as_number());
+      if (st["minflt_pool"].is_number()) timings.set("w_minflt_pool", st["minflt_pool"].as_number());
     } catch (...) {
     }
   }
