@@ -135,7 +135,9 @@ def _targets() -> List[Target]:
                 output=os.path.join(lab, "libgemmlab.so"),
                 sources=[os.path.join(lab, "gemm_lab.hip")],
                 compiler=HIPCC,
-                compile_flags=HIP_FLAGS,
+                # accumulators in the VGPR form of MFMA: the 4-wave kernel's
+                # 256 accumulators + fragments otherwise bounce through AGPR moves
+                compile_flags=HIP_FLAGS + ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
                 link_flags=[f"--offload-arch={ARCH}", "-shared", "-fPIC"],
                 headers=[os.path.join(k, "bk_common.hpp"), os.path.join(k, "gemm256_impl.hpp"), os.path.join(k, "gemm256w4_impl.hpp")],
                 hip=True,

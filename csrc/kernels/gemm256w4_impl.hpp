@@ -60,6 +60,7 @@ static_assert(4 * kEpWaveFloats * 4 <= kSmemBytes, "epilogue staging fits");
 enum : int {
   kPinOrder = 1,    // sched_barrier fences around each MFMA block
   kInterleave = 2,  // sched_group_barrier: spread ds_read / glds among the MFMAs
+  kNoCarry = 4,     // no fragment prefetch across the barrier: both k-halves read at the top of the iteration
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
@@ -244,6 +245,22 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   barrier();
 
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  if constexpr ((O & kNoCarry) != 0) {
+    // loop-carried state is the accumulators only (simpler register
+    // allocation); the first MFMAs of each K-tile wait for its first reads
+    for (int t = 0; t < nk; ++t) {
+      uint16_t* cur = smem + (t & 1) * kBuf;
+      read_frags(cur, wr, wc, lane, 0, fa0, fb0);
+      read_frags(cur, wr, wc, lane, 1, fa1, fb1);
+      mfma_block(acc, fa0, fb0);
+      mfma_block(acc, fa1, fb1);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      barrier();
+      const int kn = min(t + 2, nk - 1) * TK;
+      stage(pa, kn, cur, wave);
+      stage(pb, kn, cur + kOperand, wave);
+    }
+  } else {
   read_frags(smem, wr, wc, lane, 0, fa0, fb0);
   for (int t = 0; t < nk; ++t) {
     uint16_t* cur = smem + (t & 1) * kBuf;
@@ -269,6 +286,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
     else if constexpr (pin) __builtin_amdgcn_sched_barrier(0);
     mfma_block(acc, fa1, fb1);
     if constexpr (pin || inter) __builtin_amdgcn_sched_barrier(0);
+  }
   }
 
   // every wave's last LDS reads and tail glds retired before any wave's

@@ -21,8 +21,9 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NAMES = {0: "round1", 1: "keep_b0", 2: "round1_nostagger", 3: "keep_b0_nostagger", 4: "diag_round1_l2", 5: "diag_keep_b0_l2",
-         6: "w4", 7: "w4_pinned", 8: "w4_interleaved"}
+         6: "w4", 7: "w4_pinned", 8: "w4_interleaved", 9: "w4_nocarry"}
 DIAG = {4, 5}
+PROD = None
 
 
 def load():
@@ -69,6 +70,9 @@ def bench(lib, variants, M, N, K, rounds, reps):
     c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     fns = {NAMES[v]: (lambda v=v: run(lib, v, a, bt, c)) for v in variants}
     fns["hipblaslt"] = lambda: torch.matmul(a, bt.T, out=c)
+    if PROD is not None:  # the shipped libbeekern 256x256 kernel (built without the lab's flags)
+        fns["libbeekern_256"] = lambda: PROD.bk_gemm_bf16_tn_variant(
+            a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, N, 1.0, 0.0, 2, 3, torch.cuda.current_stream().cuda_stream)
     for f in fns.values():
         for _ in range(5):
             f()
@@ -98,6 +102,14 @@ def main():
     args = p.parse_args()
     torch.cuda.init()
     lib = load()
+    global PROD
+    try:
+        import sys as _sys
+        _sys.path.insert(0, ROOT)
+        from bee_code_interpreter_fs_amd.ops import _native
+        PROD = _native.lib()
+    except Exception:  # noqa: BLE001
+        PROD = None
     if args.one is not None:
         a = torch.empty(4096, 4096, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         bt = torch.empty(4096, 4096, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)

@@ -1,0 +1,2 @@
+source tools/gpu_steps.sh
+step gemm_lab3 400 python tools/gemm_lab.py --variants 0 1 6 8 9
