@@ -216,7 +216,8 @@ def _finish(code: int, timing_path: Optional[str] = None, sock: Optional[socket.
         # (each one is paid for on every execution)
         sys.stderr.write("NEW_MODULES " + " ".join(sorted(set(sys.modules) - ZYGOTE_MODULES)) + "\n")
         t0 = _STAMPS.get("recv", 0)
-        sys.stderr.write("STAMPS " + json.dumps({k: round(v - t0, 3) for k, v in _STAMPS.items()}) + "\n")
+        sys.stderr.write("STAMPS " + json.dumps({k: (v if k.startswith(("cpu_", "flt_", "minflt")) else round(v - t0, 3))
+                                                 for k, v in _STAMPS.items()}) + "\n")
     try:
         import atexit
 
@@ -272,9 +273,48 @@ def _prefault() -> None:
         pass
 
 
+def reseed_entropy_state() -> None:
+    """Give this sandbox its own numpy legacy RandomState stream.
+
+    A fresh interpreter (the reference's process per run) seeds numpy's
+    global RandomState from OS entropy at import; sandboxes forked from a
+    zygote would all inherit the zygote's, so every execution would draw the
+    same ``np.random.rand()`` (and scipy's default ``random_state``, which is
+    the same object).  The full 19968-bit MT19937 state is replaced from the
+    OS in one C call: ~0.4 ms less copy-on-write work than ``seed()``'s
+    SeedSequence path, and nothing that captured the object at import is
+    left on the old stream."""
+    npr = sys.modules.get("numpy.random")
+    if npr is None:
+        return
+    try:
+        import numpy as np
+
+        npr.mtrand._rand.set_state(("MT19937", np.frombuffer(os.urandom(2496), dtype=np.uint32), 624))
+    except Exception:  # keep the sandbox usable; the stream is then the zygote's
+        pass
+
+
+_DEBUG = False  # BEE_DEBUG_NEW_MODULES=1: per-phase CPU / fault stamps of the pooled phase
+
+
+def _cpu_stamp_force(name: str) -> None:
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    _STAMPS["cpu_" + name] = round((ru.ru_utime + ru.ru_stime) * 1e3, 3)
+    _STAMPS["flt_" + name] = ru.ru_minflt
+
+
+def _cpu_stamp(name: str) -> None:
+    if _DEBUG:
+        _cpu_stamp_force(name)
+
+
 def worker_main(spawn: dict) -> None:
     """Entry point in the forked child; never returns."""
+    global _DEBUG
     try:
+        _DEBUG = os.environ.get("BEE_DEBUG_NEW_MODULES") == "1"
+        _cpu_stamp("forked")
         os.setsid()
         env = spawn.get("env") or {}
         os.environ.update({k: str(v) for k, v in env.items()})
@@ -284,10 +324,14 @@ def worker_main(spawn: dict) -> None:
         sock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
         sock.connect(os.environ["BEE_WORKER_SOCK"])
         _send(sock, {"op": "hello", "id": spawn["id"], "pid": os.getpid()})
+        _cpu_stamp("hello")
+        reseed_entropy_state()
         t0 = time.perf_counter()
         warm = os.environ.get("BEE_WARM_GPU") == "1" or bool(os.environ.get("BEE_BROKER_SOCK"))
         gpu_error = warm_gpu() if warm else None
+        _cpu_stamp("warm")
         _prefault()
+        _cpu_stamp("prefault")
         _send(sock, {"op": "ready", "warm_ms": (time.perf_counter() - t0) * 1e3, "gpu_error": gpu_error or ""})
         job = _recv_line(sock)
         if job is None or job.get("op") != "run":

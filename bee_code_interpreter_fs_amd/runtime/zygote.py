@@ -19,6 +19,7 @@ orphaned by user code are reaped here too.
 
 from __future__ import annotations
 
+import _signal
 import ctypes
 import json
 import os
@@ -91,6 +92,45 @@ def _freeze_for_fork() -> None:
     worker.ZYGOTE_MODULES = frozenset(sys.modules)
 
 
+def _make_raw_fork():
+    """glibc ``fork()`` called with the GIL held, for the single-threaded
+    zygote.  ``os.fork`` additionally runs CPython's after-fork machinery in
+    the child -- ``threading._after_fork`` and the other at-fork handlers --
+    which measured ~0.7 ms and ~180 copy-on-write faults per sandbox
+    (tools/probe/worker_cost.py): state repair that only matters when other
+    threads existed at the fork.  Falls back to ``os.fork`` if the zygote has
+    more than one Python thread or ``BEE_RAW_FORK=0``."""
+    if os.environ.get("BEE_RAW_FORK", "1") == "0":
+        return None
+    import threading
+
+    if threading.active_count() != 1:
+        return None
+    try:
+        fn = ctypes.PyDLL(None, use_errno=True).fork
+    except (AttributeError, OSError):
+        return None
+    fn.restype = ctypes.c_int
+    fn.argtypes = []
+    return fn
+
+
+def _fork(raw) -> int:
+    if raw is None:
+        return os.fork()
+    pid = raw()
+    if pid < 0:
+        err = ctypes.get_errno()
+        raise OSError(err, os.strerror(err))
+    if pid == 0:
+        # the one at-fork handler whose effect sandboxes rely on: a fresh
+        # `random` stream per process (os.fork's after_in_child does this)
+        import random
+
+        random.seed()
+    return pid
+
+
 def _hip_initialized() -> bool:
     torch = sys.modules.get("torch")
     try:
@@ -118,6 +158,10 @@ def main() -> None:
 
     send({"op": "hello", "pid": os.getpid(), "preloaded": loaded, "import_ms": import_ms})
 
+    from . import worker
+
+    debug = os.environ.get("BEE_DEBUG_NEW_MODULES") == "1"
+    raw_fork = _make_raw_fork()
     rfd, wfd = os.pipe()
     os.set_blocking(wfd, False)
     signal.set_wakeup_fd(wfd)
@@ -127,6 +171,8 @@ def main() -> None:
     sel = selectors.DefaultSelector()
     sel.register(chan, selectors.EVENT_READ, "chan")
     sel.register(rfd, selectors.EVENT_READ, "sig")
+    sel_fd = sel.fileno()
+    sigchld, sigterm = int(signal.SIGCHLD), int(signal.SIGTERM)
     buf = b""
     children = set()
 
@@ -164,22 +210,26 @@ def main() -> None:
                         continue
                     t_fork = time.perf_counter()
                     try:
-                        pid = os.fork()
+                        pid = _fork(raw_fork)
                     except OSError as e:
                         send({"op": "spawn_failed", "id": msg.get("id"), "error": str(e)})
                         continue
                     if pid == 0:
                         # ---- child ----
-                        signal.set_wakeup_fd(-1)
-                        signal.signal(signal.SIGCHLD, signal.SIG_DFL)
-                        signal.signal(signal.SIGTERM, signal.SIG_DFL)
-                        sel.close()
-                        for f in (rfd, wfd):
+                        if debug:
+                            worker._cpu_stamp_force("child_entry")
+                        # drop the zygote's signal plumbing and descriptors
+                        # (the control channel above all) at C level: the
+                        # enum-wrapping `signal` helpers and selector/socket
+                        # close paths cost ~0.3 ms of copy-on-write faults
+                        _signal.set_wakeup_fd(-1)
+                        _signal.signal(sigchld, _signal.SIG_DFL)
+                        _signal.signal(sigterm, _signal.SIG_DFL)
+                        for f in (sel_fd, rfd, wfd, chan.detach()):
                             os.close(f)
-                        chan.close()
-                        from .worker import worker_main
-
-                        worker_main(msg)  # never returns
+                        if debug:
+                            worker._cpu_stamp_force("child_closed")
+                        worker.worker_main(msg)  # never returns
                         os._exit(70)
                     children.add(pid)
                     send({"op": "spawned", "id": msg.get("id"), "pid": pid, "fork_ms": (time.perf_counter() - t_fork) * 1e3})

@@ -396,3 +396,14 @@ def test_grpc_ad_hoc_import(stub):
     assert "Hello World" in r.stdout
     r = stub.Execute(pb.ExecuteRequest(source_code="import importlib.util\nprint(importlib.util.find_spec('cowsay') is None)"))
     assert r.stdout == "True\n"
+
+
+def test_sandboxes_do_not_share_rng_state(http):
+    """Each execution is a fresh sandbox, as the reference's fresh interpreter
+    per run: numpy's global RandomState and `random` are seeded per sandbox,
+    not inherited from the zygote the sandbox was forked from."""
+    for code in ("import numpy as np\nprint(np.random.rand())", "import random\nprint(random.random())",
+                 "import numpy as np, pandas\nprint(np.random.rand())",
+                 "from scipy import stats\nprint(stats.norm.rvs())"):
+        outs = [http.post("/v1/execute", json={"source_code": code, "files": {}}).json()["stdout"] for _ in range(3)]
+        assert len(set(outs)) == 3, (code, outs)

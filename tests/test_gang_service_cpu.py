@@ -1,0 +1,72 @@
+"""The multi-GPU request path end to end on CPU, with *virtual* GPU slots.
+
+bench.py's N>1 runs (the driver's 8-GPU pass) send ``Execute(gpus=N)``
+through the service: the local pool claims N slots (``_acquire_gang``),
+drains them in every daemon (``/v1/reserve`` under the node flock), and the
+lead executor starts N ranks with the rendezvous environment.  Slots here are
+GPU ids 0 and 1 on a machine without GPUs -- ``HIP_VISIBLE_DEVICES`` is only
+an environment variable to the scheduler -- and the ranks all-reduce over
+gloo instead of RCCL, so everything but the collective's transport is the
+8-GPU code path.
+"""
+
+import textwrap
+
+import pytest
+
+from .harness import ServiceHarness, ensure_native_executor
+
+GANG_GLOO = textwrap.dedent(
+    """
+    import os, torch, torch.distributed as dist
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x = torch.tensor([float(rank + 1)])
+    dist.all_reduce(x)
+    print(f"rank{rank}/{world} sum={x.item()} local={os.environ['LOCAL_RANK']} vis={os.environ.get('HIP_VISIBLE_DEVICES')}")
+    dist.destroy_process_group()
+    """
+)
+
+
+@pytest.fixture(scope="module")
+def two_slot_service(tmp_path_factory):
+    ensure_native_executor()
+    h = ServiceHarness(
+        str(tmp_path_factory.mktemp("gangsvc")),
+        gpu_ids=[0, 1],
+        broker_enabled=False,
+        worker_warm_gpu=False,
+        workers_per_gpu_target=1,
+        default_timeout=120.0,
+    )
+    h.start()
+    yield h
+    h.stop()
+
+
+def test_gang_request_spans_both_slots(two_slot_service):
+    h = two_slot_service
+    r = h.call(h.ctx.code_executor.execute(source_code=GANG_GLOO, gpus=2, nprocs=2, timeout=120), timeout=300)
+    assert r.exit_code == 0, r.stderr
+    lines = sorted(l for l in r.stdout.splitlines() if l.startswith("rank"))
+    assert len(lines) == 2, r.stdout
+    assert all("sum=3.0" in l and "vis=0,1" in l for l in lines), lines
+    assert sorted(r.gpu_ids) == [0, 1]
+
+
+def test_single_gpu_requests_spread_and_gang_after(two_slot_service):
+    """Single-GPU traffic uses both slots; a gang request afterwards still
+    gets both (reservations released, nothing left draining)."""
+    import asyncio
+
+    h = two_slot_service
+
+    async def burst():
+        return await asyncio.gather(*(h.ctx.code_executor.execute(source_code="print(6 * 7)") for _ in range(6)))
+
+    rs = h.call(burst(), timeout=300)
+    assert all(r.exit_code == 0 and r.stdout == "42\n" for r in rs)
+    assert {g for r in rs for g in r.gpu_ids} == {0, 1}
+    r = h.call(h.ctx.code_executor.execute(source_code=GANG_GLOO, gpus=2, nprocs=2, timeout=120), timeout=300)
+    assert r.exit_code == 0 and r.stdout.count("sum=3.0") == 2, (r.stdout, r.stderr)

@@ -53,8 +53,10 @@ def main():
     info = bk.device_info()
     emit(kernel="device", **info)
     n = 10**8
-    x = bk.random.rand(n)
-    ms, mn = timed(lambda: bk.random.rand(n))
+    # draws are lazy (generated on first use, fused into a consuming
+    # reduction): materialise explicitly to time the generator + HBM write
+    x = bk.random.rand(n)._materialize()
+    ms, mn = timed(lambda: bk.random.rand(n)._materialize())
     emit(kernel="philox_uniform_f64", n=n, ms=ms, min_ms=mn, GBps=n * 8 / ms / 1e6)
     tx = torch.empty(n, dtype=torch.float64, device="cuda")
     ms_t, _ = torch_timed(lambda: tx.uniform_())
@@ -71,6 +73,11 @@ def main():
     emit(kernel="square_sum_f64 fused", n=n, ms=ms, min_ms=mn, GBps=n * 8 / ms / 1e6)
     ms_t, _ = torch_timed(lambda: torch.sum(torch.square(tx)))
     emit(kernel="torch.sum(square) f64", n=n, ms=ms_t, GBps=n * 8 / ms_t / 1e6)
+
+    # the payload's lowering: sum(square(rand(n))) as ONE fused
+    # Philox->square->reduce kernel (no HBM traffic; compute-bound generator)
+    ms, mn = timed(lambda: bk.sum(bk.square(bk.random.rand(n))))
+    emit(kernel="fused rand->square->sum f64 (no HBM)", n=n, ms=ms, min_ms=mn, Gdraws_per_s=n / ms / 1e6)
 
     # whole benchmark-numpy payload on device (host wall clock, includes readback)
     for _ in range(3):

@@ -1,0 +1,42 @@
+"""What does a minimal GPU sandbox do beyond its zygote?  Runs the headline
+payload through a live service (one GPU slot) with BEE_DEBUG_NEW_MODULES=1:
+each sandbox reports the modules it imported that its zygote had not, and its
+phase stamps; prints them with the per-request timings.
+
+    python tools/probe/sandbox_debug.py [--n 5]
+"""
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=5)
+    args = ap.parse_args()
+    os.environ["BEE_DEBUG_NEW_MODULES"] = "1"
+    from tests.harness import ServiceHarness, ensure_native_executor
+
+    ensure_native_executor()
+    src = open(os.path.join(ROOT, "examples", "benchmark_numpy_gpu.py")).read()
+    h = ServiceHarness(tempfile.mkdtemp(prefix="bee-dbg-"), gpu_ids=[0], workers_per_gpu_target=1,
+                       min_workers_per_gpu_target=4, light_workers_per_gpu_target=1, default_timeout=120.0)
+    h.start()
+    try:
+        for i in range(args.n):
+            r = h.call(h.ctx.code_executor.execute(source_code=src), timeout=300)
+            lines = [l for l in r.stderr.splitlines() if l.startswith(("NEW_MODULES", "STAMPS"))]
+            print(json.dumps({"i": i, "exit": r.exit_code, "debug": lines,
+                              "timings": {k: round(v, 3) for k, v in sorted(r.timings_ms.items())}}), flush=True)
+    finally:
+        h.stop()
+
+
+if __name__ == "__main__":
+    main()
