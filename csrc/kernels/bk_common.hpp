@@ -68,6 +68,42 @@ inline unsigned stream_grid(int64_t work_items, int block, int max_blocks_per_cu
 
 inline int launch_status() { return hipGetLastError() == hipSuccess ? kOk : kLaunchFailed; }
 
+// Streaming 16-B accesses.  NT = non-temporal (nt cache policy): measured on
+// MI355X for 1e8 f64 (tools/probe/reduce_probe.hip) a square-copy went
+// 5.70 -> 6.31 TB/s with nt loads + stores and a square-sum 5.24 -> 6.65 TB/s
+// with nt loads (plus 16 loads in flight, 32 blocks/CU).  Only arrays that do
+// not fit the 256 MiB Infinity Cache take the nt path: a smaller output is
+// likely re-read from the cache by the next kernel.
+constexpr int64_t kStreamNtBytes = 256ll << 20;
+inline bool stream_nt(int64_t bytes) { return bytes >= kStreamNtBytes; }
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+
+template <bool NT, typename V>
+__device__ __forceinline__ V ld16(const V* p) {
+  static_assert(sizeof(V) == 16, "16-byte accesses only");
+  if constexpr (NT) {
+    u32x4_t r = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    V v;
+    __builtin_memcpy(&v, &r, 16);
+    return v;
+  } else {
+    return *p;
+  }
+}
+
+template <bool NT, typename V>
+__device__ __forceinline__ void st16(V* p, const V& v) {
+  static_assert(sizeof(V) == 16, "16-byte accesses only");
+  if constexpr (NT) {
+    u32x4_t r;
+    __builtin_memcpy(&r, &v, 16);
+    __builtin_nontemporal_store(r, reinterpret_cast<u32x4_t*>(p));
+  } else {
+    *p = v;
+  }
+}
+
 // 64-lane wave reduction (DPP/ds_swizzle lowering of __shfl_xor).
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {

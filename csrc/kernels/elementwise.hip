@@ -1,7 +1,8 @@
 // Elementwise kernels (square, unary math, binary arithmetic, casts).
 //
 // HBM-bound: every lane moves 16 bytes per access (f64x2 / f32x4 / bf16x8,
-// Guideline 13), grid-stride over <= 8 blocks per CU.  bf16 math runs in f32
+// Guideline 13), non-temporal for arrays past the Infinity Cache
+// (bk_common.hpp ld16/st16), grid-stride over <= 64 blocks per CU.  bf16 math runs in f32
 // and rounds once on store.  `numpy.square` of the benchmark payload
 // (`examples/benchmark-numpy.py:21`) is kUnarySquare on f64.
 #include "bk_common.hpp"
@@ -66,7 +67,7 @@ struct alignas(16) Vec {
 
 constexpr int kEwUnroll = 4;  // 16-B loads in flight per lane before the first store
 
-template <typename T, int OP>
+template <typename T, int OP, bool NT>
 __global__ __launch_bounds__(256) void unary_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n) {
   using E = Elem<T>;
   using V = Vec<T>;
@@ -84,13 +85,13 @@ __global__ __launch_bounds__(256) void unary_kernel(const T* __restrict__ x, T* 
     const int64_t base = cb * chunk + threadIdx.x;
     V a[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) a[u] = xv[base + u * blockDim.x];
+    for (int u = 0; u < U; ++u) a[u] = ld16<NT>(xv + base + u * blockDim.x);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < N; ++j) a[u].v[j] = E::store(unary<OP>(E::load(a[u].v[j])));
 #pragma unroll
-    for (int u = 0; u < U; ++u) yv[base + u * blockDim.x] = a[u];
+    for (int u = 0; u < U; ++u) st16<NT>(yv + base + u * blockDim.x, a[u]);
   }
   for (int64_t i = nfull * chunk + tid; i < nvec; i += stride) {
     V a = xv[i];
@@ -103,7 +104,7 @@ __global__ __launch_bounds__(256) void unary_kernel(const T* __restrict__ x, T* 
 
 // y = op(a, b) with b an array (B_SCALAR=false) or a scalar (B_SCALAR=true);
 // REVERSED swaps the operands for scalar ops (s - x, s / x, ...).
-template <typename T, int OP, bool B_SCALAR, bool REVERSED>
+template <typename T, int OP, bool B_SCALAR, bool REVERSED, bool NT>
 __global__ __launch_bounds__(256) void binary_kernel(const T* __restrict__ a, const T* __restrict__ b, double s,
                                                      T* __restrict__ y, int64_t n) {
   using E = Elem<T>;
@@ -133,13 +134,13 @@ __global__ __launch_bounds__(256) void binary_kernel(const T* __restrict__ a, co
     V va[U], vb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      va[u] = av[base + u * blockDim.x];
-      if constexpr (!B_SCALAR) vb[u] = bv[base + u * blockDim.x];
+      va[u] = ld16<NT>(av + base + u * blockDim.x);
+      if constexpr (!B_SCALAR) vb[u] = ld16<NT>(bv + base + u * blockDim.x);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) apply(va[u], vb[u]);
 #pragma unroll
-    for (int u = 0; u < U; ++u) yv[base + u * blockDim.x] = va[u];
+    for (int u = 0; u < U; ++u) st16<NT>(yv + base + u * blockDim.x, va[u]);
   }
   for (int64_t i = nfull * chunk + tid; i < nvec; i += stride) {
     V va = av[i], vb;
@@ -180,7 +181,9 @@ __global__ __launch_bounds__(256) void fill_kernel(uint8_t* __restrict__ y, int6
 // ---- host dispatch ---------------------------------------------------------
 template <typename T, int OP>
 int launch_unary_t(const void* x, void* y, int64_t n, hipStream_t s) {
-  unary_kernel<T, OP><<<stream_grid((n + Vec<T>::N - 1) / Vec<T>::N, 256), 256, 0, s>>>((const T*)x, (T*)y, n);
+  const unsigned g = stream_grid((n + Vec<T>::N - 1) / Vec<T>::N, 256);
+  if (stream_nt(n * (int64_t)sizeof(T))) unary_kernel<T, OP, true><<<g, 256, 0, s>>>((const T*)x, (T*)y, n);
+  else unary_kernel<T, OP, false><<<g, 256, 0, s>>>((const T*)x, (T*)y, n);
   return launch_status();
 }
 
@@ -193,8 +196,11 @@ int dispatch_unary(int op, const void* x, void* y, int64_t n, hipStream_t s, std
 
 template <typename T, int OP, bool BS, bool REV>
 int launch_binary_t(const void* a, const void* b, double sc, void* y, int64_t n, hipStream_t s) {
-  binary_kernel<T, OP, BS, REV>
-      <<<stream_grid((n + Vec<T>::N - 1) / Vec<T>::N, 256), 256, 0, s>>>((const T*)a, (const T*)b, sc, (T*)y, n);
+  const unsigned g = stream_grid((n + Vec<T>::N - 1) / Vec<T>::N, 256);
+  if (stream_nt(n * (int64_t)sizeof(T)))
+    binary_kernel<T, OP, BS, REV, true><<<g, 256, 0, s>>>((const T*)a, (const T*)b, sc, (T*)y, n);
+  else
+    binary_kernel<T, OP, BS, REV, false><<<g, 256, 0, s>>>((const T*)a, (const T*)b, sc, (T*)y, n);
   return launch_status();
 }
 

@@ -12,6 +12,7 @@
 namespace bk {
 
 // out[i] = U[0,1) (f64), scaled to [lo, hi).  Each counter value -> 2 doubles.
+template <bool NT>
 __global__ __launch_bounds__(256) void philox_uniform_f64(double* __restrict__ out, int64_t n, uint32_t k0,
                                                           uint32_t k1, uint64_t offset, double lo, double span) {
   const int64_t pairs = (n + 1) / 2;
@@ -22,7 +23,7 @@ __global__ __launch_bounds__(256) void philox_uniform_f64(double* __restrict__ o
     double2 v = make_double2(lo + span * u53(r.x, r.y), lo + span * u53(r.z, r.w));
     const int64_t i = 2 * p;
     if (i + 1 < n) {
-      *reinterpret_cast<double2*>(out + i) = v;  // 16-B store
+      st16<NT>(reinterpret_cast<double2*>(out + i), v);  // 16-B store
     } else {
       out[i] = v.x;
     }
@@ -30,6 +31,7 @@ __global__ __launch_bounds__(256) void philox_uniform_f64(double* __restrict__ o
 }
 
 // f32: each counter value -> 4 floats, one 16-B store.
+template <bool NT>
 __global__ __launch_bounds__(256) void philox_uniform_f32(float* __restrict__ out, int64_t n, uint32_t k0, uint32_t k1,
                                                           uint64_t offset, float lo, float span) {
   const int64_t quads = (n + 3) / 4;
@@ -40,7 +42,7 @@ __global__ __launch_bounds__(256) void philox_uniform_f32(float* __restrict__ ou
     float4 v = make_float4(lo + span * u24(r.x), lo + span * u24(r.y), lo + span * u24(r.z), lo + span * u24(r.w));
     const int64_t i = 4 * q;
     if (i + 3 < n) {
-      *reinterpret_cast<float4*>(out + i) = v;
+      st16<NT>(reinterpret_cast<float4*>(out + i), v);
     } else {
       const float t[4] = {v.x, v.y, v.z, v.w};
       for (int j = 0; i + j < n; ++j) out[i + j] = t[j];
@@ -132,15 +134,20 @@ BK_API int bk_rand_uniform(void* out, int64_t n, int dtype, uint64_t seed, uint6
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   if (dtype == kF64) {
     const int64_t pairs = (n + 1) / 2;
-    philox_uniform_f64<<<stream_grid(pairs, 256), 256, 0, stream>>>((double*)out, n, k0, k1, offset, lo, hi - lo);
+    const unsigned g = stream_grid(pairs, 256);
+    if (stream_nt(n * 8)) philox_uniform_f64<true><<<g, 256, 0, stream>>>((double*)out, n, k0, k1, offset, lo, hi - lo);
+    else philox_uniform_f64<false><<<g, 256, 0, stream>>>((double*)out, n, k0, k1, offset, lo, hi - lo);
   } else if (dtype == kBF16) {
     const int64_t octs = (n + 7) / 8;
     philox_uniform_bf16<<<stream_grid(octs, 256), 256, 0, stream>>>((uint16_t*)out, n, k0, k1, offset, (float)lo,
                                                                      (float)(hi - lo));
   } else if (dtype == kF32) {
     const int64_t quads = (n + 3) / 4;
-    philox_uniform_f32<<<stream_grid(quads, 256), 256, 0, stream>>>((float*)out, n, k0, k1, offset, (float)lo,
-                                                                    (float)(hi - lo));
+    const unsigned g = stream_grid(quads, 256);
+    if (stream_nt(n * 4))
+      philox_uniform_f32<true><<<g, 256, 0, stream>>>((float*)out, n, k0, k1, offset, (float)lo, (float)(hi - lo));
+    else
+      philox_uniform_f32<false><<<g, 256, 0, stream>>>((float*)out, n, k0, k1, offset, (float)lo, (float)(hi - lo));
   } else {
     return kBadArgument;
   }

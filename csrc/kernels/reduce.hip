@@ -3,7 +3,8 @@
 // (`examples/benchmark-numpy.py:21`) is kRedSquareSum on f64 — one HBM pass
 // (800 MB read for 1e8 f64) instead of numpy's write-then-read of x².
 //
-// Stage 1: <= 4 blocks per CU, each lane streams 16-B vectors (4 in flight),
+// Stage 1: <= 32 blocks per CU, each lane streams 16-B vectors (16 in flight,
+// non-temporal past the Infinity Cache),
 // accumulates in f64, wave-reduces over 64 lanes (DPP) -> LDS -> one partial
 // per block.  Stage 2: one block folds the partials in a fixed order.  No
 // float atomics, so results are bitwise reproducible run to run.
@@ -15,7 +16,13 @@ namespace bk {
 enum ReduceOp : int { kRedSum = 0, kRedSquareSum, kRedAbsSum, kRedMax, kRedMin, kRedDot, kRedCount };
 
 constexpr int kRedBlock = 256;
-constexpr int kRedMaxBlocks = 1024;  // 4 per CU; also the workspace length
+// stage-1 grid cap, and the workspace length: 32 blocks per CU with 16 loads
+// in flight per lane (tools/probe/reduce_probe.hip: 1e8 f64 square-sum
+// 152 -> 120 us, 5.2 -> 6.6 TB/s, with non-temporal loads)
+constexpr int kRedMaxBlocks = 8192;
+constexpr int kRedUnroll = 16;
+// the fused RNG->reduce kernels are compute-bound: 4 blocks per CU
+constexpr int kRandRedMaxBlocks = 1024;
 
 template <typename T> __device__ __forceinline__ double to_f64(T v);
 template <> __device__ __forceinline__ double to_f64<double>(double v) { return v; }
@@ -62,12 +69,12 @@ template <int OP> __device__ __forceinline__ double block_reduce(double v) {
 
 template <typename T> struct alignas(16) V16 { T v[16 / sizeof(T)]; };
 
-template <typename T, int OP>
+template <typename T, int OP, bool NT>
 __global__ __launch_bounds__(kRedBlock) void reduce_stage1(const T* __restrict__ a, const T* __restrict__ b, int64_t n,
                                                           double* __restrict__ partials) {
   using V = V16<T>;
   constexpr int N = 16 / sizeof(T);
-  constexpr int U = 4;  // 16-B loads in flight per lane
+  constexpr int U = kRedUnroll;  // 16-B loads in flight per lane
   const int64_t nvec = n / N;
   const int64_t stride = (int64_t)gridDim.x * kRedBlock;
   const int64_t tid = (int64_t)blockIdx.x * kRedBlock + threadIdx.x;
@@ -80,8 +87,8 @@ __global__ __launch_bounds__(kRedBlock) void reduce_stage1(const T* __restrict__
     V va[U], vb[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      va[u] = reinterpret_cast<const V*>(a)[i + u * stride];
-      if constexpr (OP == kRedDot) vb[u] = reinterpret_cast<const V*>(b)[i + u * stride];
+      va[u] = ld16<NT>(reinterpret_cast<const V*>(a) + i + u * stride);
+      if constexpr (OP == kRedDot) vb[u] = ld16<NT>(reinterpret_cast<const V*>(b) + i + u * stride);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -183,7 +190,10 @@ int launch_reduce(const void* a, const void* b, int64_t n, double* workspace, do
   int64_t lanes_needed = (n / N + 3) / 4;  // 4 vectors per lane minimum before adding blocks
   unsigned g = stream_grid(lanes_needed > 0 ? lanes_needed : 1, kRedBlock, kRedMaxBlocks / kNumCU);
   if (g > (unsigned)kRedMaxBlocks) g = kRedMaxBlocks;  // the workspace holds kRedMaxBlocks partials
-  reduce_stage1<T, OP><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace);
+  if (stream_nt(n * (int64_t)sizeof(T) * (OP == kRedDot ? 2 : 1)))
+    reduce_stage1<T, OP, true><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace);
+  else
+    reduce_stage1<T, OP, false><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace);
   reduce_stage2<OP><<<1, kRedBlock, 0, s>>>(workspace, (int)g, out);
   return launch_status();
 }
@@ -209,8 +219,8 @@ BK_API int bk_rand_reduce(int op, int dtype, int64_t n, uint64_t seed, uint64_t 
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const int64_t units = dtype == kF64 ? (n + 1) / 2 : (n + 3) / 4;
   // fixed grid for a given n: results are reproducible run to run
-  unsigned g = stream_grid(units > 0 ? (units + 7) / 8 : 1, kRedBlock, kRedMaxBlocks / kNumCU);
-  if (g > (unsigned)kRedMaxBlocks) g = kRedMaxBlocks;
+  unsigned g = stream_grid(units > 0 ? (units + 7) / 8 : 1, kRedBlock, kRandRedMaxBlocks / kNumCU);
+  if (g > (unsigned)kRandRedMaxBlocks) g = kRandRedMaxBlocks;
   double* ws = (double*)workspace;
   if (dtype == kF64) {
     if (op == kRedSum) rand_reduce_f64<kRedSum><<<g, kRedBlock, 0, stream>>>(n, k0, k1, offset, lo, hi - lo, ws);

@@ -1,0 +1,3 @@
+source tools/gpu_steps.sh
+step gputests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
+step bench 300 python bench.py --steps 100
