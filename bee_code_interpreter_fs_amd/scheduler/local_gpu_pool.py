@@ -262,7 +262,9 @@ class LocalGpuPoolBackend(CodeExecutor):
                 body["source_file"] = request.source_file
             else:
                 body["source_code"] = request.source_code
-            if lead.gpu is not None and not gang:
+            if not gang:
+                # CPU-only slots too: their executors keep minimal (numpy-only,
+                # fast-forking) and light zygotes as well
                 body["mode"] = sandbox_mode(request, self.storage)
             if gang:
                 body["gpus"] = ",".join(str(s.gpu) for s in slots)
