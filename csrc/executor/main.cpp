@@ -189,6 +189,16 @@ int main(int argc, char** argv) {
       }
       return;
     }
+    if (req.method == "POST" && p == "/v1/shutdown" && !pool.config().pod_mode) {
+      // graceful stop requested by the owner of the (Unix) socket; used where
+      // signals are not ours to handle (rocprofv3 installs its own SIGTERM
+      // handler in the profiled daemon: tools/prof_served.sh)
+      Json j = Json::object();
+      j.set("stopping", true);
+      resp.json(200, j.dump());
+      if (g_server) g_server->stop();
+      return;
+    }
     if (req.method == "GET" && p == "/metrics") {
       resp.status = 200;
       resp.content_type = "text/plain; version=0.0.4";
