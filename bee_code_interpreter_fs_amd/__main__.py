@@ -56,9 +56,18 @@ async def _serve(ctx: ApplicationContext, stop: asyncio.Event) -> None:
     http = uvicorn.Server(uvicorn.Config(ctx.http_server, host=host, port=port, loop="asyncio", log_level="warning"))
     http.install_signal_handlers = lambda: None  # handled by the caller
     sock = _reuseport_socket(host, port)
-    await ctx.grpc_server.start(ctx.config.grpc_listen_addr)
+    ctx.grpc_server.bind(ctx.config.grpc_listen_addr)
+    private = ""
+    if os.environ.get("BEE_FRONTEND_INDEX") is not None:
+        # a replica also listens on a port of its own, so a client (or an L4
+        # balancer) can spread connections evenly instead of by SO_REUSEPORT's
+        # 4-tuple hash, which leaves some replicas with several times the
+        # connections of others
+        ghost, _ = _split_addr(ctx.config.grpc_listen_addr)
+        private = f" replica_grpc={ghost}:{ctx.grpc_server.bind(f'{ghost}:0')}"
+    await ctx.grpc_server.start()
     http_task = asyncio.create_task(http.serve(sockets=[sock]))
-    print(f"BEE_SERVICE_READY grpc={ctx.config.grpc_listen_addr} http={ctx.config.http_listen_addr}", flush=True)
+    print(f"BEE_SERVICE_READY grpc={ctx.config.grpc_listen_addr} http={ctx.config.http_listen_addr}{private}", flush=True)
     try:
         await stop.wait()
     finally:
@@ -114,13 +123,17 @@ async def supervise(config: Config, n_frontends: int) -> None:
         e = dict(env, BEE_FRONTEND_INDEX=str(i))
         children.append(subprocess.Popen([sys.executable, "-m", "bee_code_interpreter_fs_amd"], env=e, stdout=subprocess.PIPE))
     loop = asyncio.get_running_loop()
+    replicas = []
     for c in children:  # wait until every replica serves
         line = await loop.run_in_executor(None, c.stdout.readline)
         if not line.startswith(b"BEE_SERVICE_READY"):
             raise RuntimeError(f"front-end replica failed to start: {line!r}")
+        for part in line.decode().split():
+            if part.startswith("replica_grpc="):
+                replicas.append(part.split("=", 1)[1])
     print(
         f"BEE_SERVICE_READY grpc={ghost}:{gport} http={hhost}:{hport} frontends={n_frontends} "
-        f"slots={json.loads(backend.attach_spec())!r}",
+        f"replicas={','.join(replicas)} slots={json.dumps(json.loads(backend.attach_spec()), separators=(',', ':'))}",
         flush=True,
     )
     stop = _install_stop(loop)

@@ -167,7 +167,13 @@ def start_service(tmp: str, n_gpus: int, args):
         proc.kill()
         tail = open(os.path.join(tmp, "service.log"), "rb").read()[-3000:].decode(errors="replace")
         raise RuntimeError(f"service failed to start: {line!r}\n{tail}")
-    return proc, gport, hport, frontends
+    # replicas' own ports: clients are spread over them evenly (as an L4
+    # balancer would) instead of by SO_REUSEPORT's connection hash
+    replicas = []
+    for part in line.decode().split():
+        if part.startswith("replicas=") and part != "replicas=":
+            replicas = part.split("=", 1)[1].split(",")
+    return proc, gport, hport, frontends, replicas
 
 
 async def client_loop(target, pb, source, n, out):
@@ -200,11 +206,16 @@ async def client_loop(target, pb, source, n, out):
                 errors.append(f"exit={r.exit_code} stdout={r.stdout[-200:]!r} stderr={r.stderr[-500:]!r}")
 
 
-async def run_clients(target, source, concurrency, n):
+async def run_clients(targets, first_client, source, concurrency, n):
+    """``concurrency`` closed-loop clients; global client g connects to
+    targets[g % len(targets)] (the front-end replicas, round-robin over all
+    ranks' clients)."""
     from bee_code_interpreter_fs_amd.models import proto as pb
 
     out = ([], [], [], {})
-    await asyncio.gather(*(client_loop(target, pb, source, n, out) for _ in range(concurrency)))
+    await asyncio.gather(
+        *(client_loop(targets[(first_client + i) % len(targets)], pb, source, n, out) for i in range(concurrency))
+    )
     return out
 
 
@@ -288,21 +299,24 @@ def main():
     loop = asyncio.new_event_loop()
     proc = None
     tmp = tempfile.mkdtemp(prefix="bee-bench-", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
-    info = [None, None, None]
+    info = [None, None, None, None]
     try:
         if rank == 0:
-            proc, gport, hport, frontends = start_service(tmp, n_gpus, args)
-            info = [gport, hport, frontends]
+            proc, gport, hport, frontends, replicas = start_service(tmp, n_gpus, args)
+            info = [gport, hport, frontends, replicas]
         if world > 1:
             dist.broadcast_object_list(info, src=0)
-        gport, hport, frontends = info
+        gport, hport, frontends, replicas = info
         target = f"127.0.0.1:{gport}"
+        targets = replicas or [target]
+        first = rank * args.concurrency
 
-        loop.run_until_complete(run_clients(target, source, args.concurrency, args.warmup))  # warm every pool
+        loop.run_until_complete(run_clients(targets, first, source, args.concurrency, args.warmup))  # warm every pool
         barrier()
         cpu0, cpu_src = cpu_usage_s()
         t0 = time.perf_counter()
-        lat, errors, exec_times, phases = loop.run_until_complete(run_clients(target, source, args.concurrency, args.steps))
+        lat, errors, exec_times, phases = loop.run_until_complete(
+            run_clients(targets, first, source, args.concurrency, args.steps))
         barrier()
         elapsed = time.perf_counter() - t0
         cpu_busy = (cpu_usage_s()[0] - cpu0) / elapsed if elapsed > 0 else 0.0
@@ -347,7 +361,8 @@ def main():
                     "global_batch": args.concurrency * world,
                     "seq_len": None,
                     "parallelism": f"{n_gpus} {'CPU-only' if args.cpu_only else 'GPU-pinned'} executor pods, {frontends} front-end replicas, "
-                    f"{args.concurrency * world} concurrent clients",
+                    f"{args.concurrency * world} concurrent clients"
+                    + (f" (round-robin over the {len(replicas)} replica ports)" if replicas else ""),
                     "execution": "every Execute runs in its own single-use sandbox process on the pinned GPU; "
                     "beekern draws are lazy, so sum(square(rand(1e8))) lowers to one fused Philox->square->reduce "
                     "kernel (the unobserved draw never round-trips HBM; set BEE_LAZY_RANDOM=0 to materialise it)",
