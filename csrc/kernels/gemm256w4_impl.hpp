@@ -61,6 +61,7 @@ enum : int {
   kPinOrder = 1,    // sched_barrier fences around each MFMA block
   kInterleave = 2,  // sched_group_barrier: spread ds_read / glds among the MFMAs
   kNoCarry = 4,     // no fragment prefetch across the barrier: both k-halves read at the top of the iteration
+  kDirectStore = 8, // epilogue: each lane stores its accumulators straight to C (no LDS staging)
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
@@ -293,7 +294,25 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   // staging writes
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   barrier();
-  epilogue<OUT_BF16>(smem, acc, C, ldc, m0 + wr * 128, n0 + wc * 128, wave, lane, alpha, beta);
+  if constexpr ((O & kDirectStore) != 0) {
+    // 16x16 C/D map: lane holds rows 4*(lane/16)+r of column lane%16 -> 4
+    // scattered element stores per fragment (f32 output only; cheap on
+    // registers, expensive on store issue)
+    const int64_t r0 = m0 + wr * 128, c0 = n0 + wc * 128;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = r0 + i * 16 + (lane >> 4) * 4 + r;
+          const int col = c0 + j * 16 + (lane & 15);
+          if constexpr (OUT_BF16) ((uint16_t*)C)[row * ldc + col] = float_to_bf16_bits(alpha * acc[i][j][r]);
+          else ((float*)C)[row * ldc + col] = alpha * acc[i][j][r] + (beta != 0.f ? beta * ((float*)C)[row * ldc + col] : 0.f);
+        }
+  } else {
+    epilogue<OUT_BF16>(smem, acc, C, ldc, m0 + wr * 128, n0 + wc * 128, wave, lane, alpha, beta);
+  }
 }
 
 inline bool ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16) {

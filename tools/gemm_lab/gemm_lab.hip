@@ -23,7 +23,7 @@ void run(const void* A, const void* B, void* C, int M, int N, int K, int lda, in
 }  // namespace
 
 // 4-wave 128x128-per-wave kernel options, lab ids 6..
-constexpr int kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave, g4::kNoCarry};
+constexpr int kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave, g4::kNoCarry, g4::kDirectStore};
 template <int I>
 void run_w4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool bf,
             hipStream_t s) {
@@ -47,6 +47,7 @@ BK_API int gemmlab_run(int variant, const void* A, const void* Bt, void* C, int 
     case 7: run_w4<1>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 8: run_w4<2>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 9: run_w4<3>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 10: run_w4<4>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     default: return kBadArgument;
   }
   return launch_status();
