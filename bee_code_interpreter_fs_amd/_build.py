@@ -144,6 +144,21 @@ def _targets() -> List[Target]:
                 optional=True,
             )
         )
+    zl = os.path.join(CSRC, "zygote")
+    if os.path.isdir(zl):
+        import sysconfig
+
+        targets.append(
+            Target(
+                name="zygote-loop",
+                output=os.path.join(PKG, "runtime", "_zygote_loop" + sysconfig.get_config_var("EXT_SUFFIX")),
+                sources=[os.path.join(zl, "zygote_loop.cpp")],
+                compiler=CXX,
+                compile_flags=["-O2", "-fPIC", "-std=c++17", "-Wall", "-Wextra", "-Wno-missing-field-initializers",
+                               f"-I{sysconfig.get_paths()['include']}"],
+                link_flags=["-shared", "-fPIC"],
+            )
+        )
     if os.path.isdir(rb) and os.listdir(rb):
         targets.append(
             Target(

@@ -139,6 +139,18 @@ def _hip_initialized() -> bool:
         return False
 
 
+def _native_loop():
+    """The C control loop (``_zygote_loop``, built in-tree), unless
+    ``BEE_ZYGOTE_PYLOOP=1`` or it is not built."""
+    if os.environ.get("BEE_ZYGOTE_PYLOOP") == "1":
+        return None
+    try:
+        from . import _zygote_loop
+    except ImportError:
+        return None
+    return _zygote_loop
+
+
 def main() -> None:
     fd = int(os.environ["BEE_ZYGOTE_FD"])
     chan = socket.socket(fileno=fd)
@@ -162,6 +174,22 @@ def main() -> None:
 
     debug = os.environ.get("BEE_DEBUG_NEW_MODULES") == "1"
     raw_fork = _make_raw_fork()
+    native = _native_loop() if raw_fork is not None else None
+    if native is not None:
+        # the per-request loop runs in C (csrc/zygote/zygote_loop.cpp); Python
+        # runs again only in a forked child, handed its spawn line
+        line = native.serve(chan.fileno())
+        if line is None:
+            return  # channel closed / SIGTERM: the loop killed its sandboxes
+        chan.detach()  # the loop closed the descriptor in the child
+        if debug:
+            worker._cpu_stamp_force("child_entry")
+        import random
+
+        random.seed()  # what os.fork's after-fork handler would have done
+        worker.worker_main(json.loads(line))  # never returns
+        os._exit(70)
+
     rfd, wfd = os.pipe()
     os.set_blocking(wfd, False)
     signal.set_wakeup_fd(wfd)
