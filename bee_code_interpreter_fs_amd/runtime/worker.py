@@ -255,6 +255,30 @@ def _finish(code: int, timing_path: Optional[str] = None, sock: Optional[socket.
     os._exit(status)
 
 
+_LIGHT_WARMUP = """
+import numpy as np, pandas as pd
+df = pd.DataFrame({"a": np.arange(64.0), "b": np.arange(64.0)[::-1]})
+df["c"] = df["a"] * 2 + df["b"]
+s = df.describe().loc[["mean", "std"]].to_string()
+"""
+
+
+def _prefault_scientific() -> None:
+    """Light sandboxes (pandas / scipy preloaded): touch the common
+    DataFrame construction / arithmetic / describe / printing paths while
+    pooled.  A light
+    sandbox's first pandas call otherwise pays thousands of copy-on-write
+    faults on the request path (the objects it touches are the zygote's)."""
+    if os.environ.get("BEE_ZYGOTE_KIND") != "light" or "pandas" not in sys.modules:
+        return
+    if os.environ.get("BEE_LIGHT_WARMUP", "1") == "0":
+        return
+    try:
+        exec(compile(_LIGHT_WARMUP, "<light-warmup>", "exec", dont_inherit=True), {"__name__": "__warmup__"})
+    except Exception:
+        pass
+
+
 def _prefault() -> None:
     """Run the request path's Python machinery once while the sandbox waits
     in the pool: a freshly forked process pays a copy-on-write fault on every
@@ -331,6 +355,7 @@ def worker_main(spawn: dict) -> None:
         gpu_error = warm_gpu() if warm else None
         _cpu_stamp("warm")
         _prefault()
+        _prefault_scientific()
         _cpu_stamp("prefault")
         _send(sock, {"op": "ready", "warm_ms": (time.perf_counter() - t0) * 1e3, "gpu_error": gpu_error or ""})
         job = _recv_line(sock)

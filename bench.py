@@ -59,6 +59,12 @@ WORKLOADS = {
         "benchmark-fib.py payload: 1000 x fib(10000) Python bigint per Execute",
         "python int",
     ),
+    "scientific": (
+        "examples/scientific_stack.py",
+        "Execute RPCs/sec (numpy/pandas/scipy t-test payload, light sandboxes)",
+        "using_imports-style payload: pandas DataFrame describe + scipy.stats t-test per Execute",
+        "float64",
+    ),
     "hello": (
         "examples/hello_world.py",
         "Execute RPCs/sec (hello_world plumbing)",
@@ -148,7 +154,10 @@ def start_service(tmp: str, n_gpus: int, args):
             "APP_WORKERS_PER_GPU_TARGET": "1",  # direct sandboxes: the payload does not need them
             # the payloads import only beekern/numpy/stdlib -> minimal sandboxes
             "APP_MIN_WORKERS_PER_GPU_TARGET": str(args.pool_target),
-            "APP_LIGHT_WORKERS_PER_GPU_TARGET": "4",
+            # light sandboxes (pandas/scipy/matplotlib preloaded) serve the
+            # scientific workload; the others only keep a few warm
+            "APP_LIGHT_WORKERS_PER_GPU_TARGET": str(args.pool_target if args.workload == "scientific" else 4),
+            "APP_LIGHT_ZYGOTES_PER_GPU": "4" if args.workload == "scientific" else "2",
             "APP_MAX_INFLIGHT_PER_GPU": str(max(args.concurrency * 2, 8)),
             "APP_DEFAULT_TIMEOUT": "300",
             "APP_FRONTEND_PROCESSES": str(frontends),

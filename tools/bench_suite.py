@@ -24,6 +24,7 @@ RUNS = [
     ("fib_gpu_pod", ["--workload", "fib", "--steps", "4", "--concurrency", "16"]),
     ("numpy_gpu", ["--workload", "numpy_gpu", "--steps", "30"]),
     ("numpy_cpu", ["--workload", "numpy_cpu", "--steps", "3", "--concurrency", "4"]),
+    ("scientific_gpu_pod", ["--workload", "scientific", "--steps", "30"]),
 ]
 
 
