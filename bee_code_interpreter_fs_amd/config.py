@@ -93,6 +93,10 @@ class Config:
     min_workers_per_gpu_target: int = 16
     # zygote processes forking minimal sandboxes per GPU
     min_zygotes_per_gpu: int = 4
+    # warm minimal sandboxes per GPU for scripts that import no GPU module:
+    # their kernel-broker session opens only if used (-1 = as many as the
+    # minimal pool)
+    min_cpu_workers_per_gpu_target: int = -1
     # run the per-GPU kernel broker in the executor daemon
     broker_enabled: bool = True
     # zygote processes forking light sandboxes per GPU (fork parallelism)

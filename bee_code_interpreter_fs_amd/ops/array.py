@@ -58,16 +58,21 @@ def normalize_dtype(dtype: Any) -> str:
     return name
 
 
-def init(device: Optional[int] = None) -> int:
+def init(device: Optional[int] = None, lazy: bool = False) -> int:
     """Initialise the driver (HIP context on ``device``, or a broker session);
-    idempotent.  Sandboxes do this while waiting in the warm pool."""
+    idempotent.  Sandboxes do this while waiting in the warm pool.  ``lazy``
+    (broker driver only) defers opening the session to the first request."""
     global _driver
     if _driver is not None:
         return _driver.device
     with _state_lock:
         if _driver is None:
             d = make_driver()
-            d.init(int(os.environ.get("BEE_DEVICE", "0")) if device is None else int(device))
+            dev = int(os.environ.get("BEE_DEVICE", "0")) if device is None else int(device)
+            if lazy and d.name == "broker":
+                d.init(dev, lazy=True)
+            else:
+                d.init(dev)
             _driver = d
     return _driver.device
 

@@ -173,7 +173,15 @@ class BrokerDriver:
         self.quota = 0
         self.arch = ""
 
-    def init(self, device: int) -> None:
+    def init(self, device: int, lazy: bool = False) -> None:
+        """Open the broker session (connect + HELLO); with ``lazy`` the
+        session opens on the first request instead, so a sandbox that never
+        touches the GPU costs the broker nothing."""
+        self.device = device
+        if not lazy:
+            self._connect()
+
+    def _connect(self) -> None:
         s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
         s.connect(self.path)
         self.sock = s
@@ -181,7 +189,6 @@ class BrokerDriver:
         (self.quota,) = struct.unpack_from("<q", payload, 0)
         (n,) = struct.unpack_from("<I", payload, 8)
         self.arch = payload[12 : 12 + n].decode()
-        self.device = device
 
     def _recv_into(self, view: memoryview) -> None:
         got = 0
@@ -192,6 +199,8 @@ class BrokerDriver:
             got += k
 
     def _call(self, op: int, payload: bytes, out: Optional[memoryview] = None) -> bytes:
+        if self.sock is None and op != HELLO:
+            self._connect()
         hdr = _HDR.pack(op, 0, len(payload))
         with self.lock:
             if len(payload) < (1 << 16):
@@ -224,6 +233,8 @@ class BrokerDriver:
         """Fire-and-forget request (kernel launches, frees): no reply; a
         failure is raised by the next request that waits for one (sync,
         reduce, read, alloc) -- the asynchronous-error model of GPU streams."""
+        if self.sock is None:
+            self._connect()
         with self.lock:
             self.sock.sendall(_HDR.pack(op, _NO_REPLY, len(payload)) + payload)
 

@@ -132,7 +132,9 @@ def warm_gpu() -> Optional[str]:
     try:
         from bee_code_interpreter_fs_amd import ops
 
-        ops.init(0)
+        # BEE_BROKER_LAZY=1: a light/minimal sandbox opens its broker session
+        # on first use instead of while pooled
+        ops.init(0, lazy=os.environ.get("BEE_BROKER_LAZY") == "1")
         quota = int(os.environ.get("BEE_HBM_QUOTA_BYTES", "0") or 0)
         if quota > 0 and ops.driver_name() == "native":
             ops.set_quota(quota)

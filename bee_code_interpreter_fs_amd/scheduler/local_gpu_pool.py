@@ -142,7 +142,8 @@ class LocalGpuPoolBackend(CodeExecutor):
             broker=c.broker_enabled,
             light_zygotes=c.light_zygotes_per_gpu,
             extra_args=["--max-idle", str(c.worker_max_idle_s), "--min-target", str(c.min_workers_per_gpu_target),
-                        "--min-zygotes", str(c.min_zygotes_per_gpu)],
+                        "--min-zygotes", str(c.min_zygotes_per_gpu),
+                        "--min-cpu-target", str(c.min_cpu_workers_per_gpu_target)],
         )
 
     async def wait_ready(self, timeout: float = 300.0) -> None:
@@ -418,13 +419,17 @@ def sandbox_mode(request: ExecuteRequest, storage: Storage) -> str:
     if DIRECT_GPU_MODULES.intersection(mods):
         return "direct"
     if all(m in MIN_MODULES or m in _STDLIB for m in mods):
-        return "min"  # numpy/beekern/stdlib only: the fast-forking minimal zygote
+        # numpy/beekern/stdlib only: the fast-forking minimal zygote; scripts
+        # that never import beekern take a sandbox whose broker session opens
+        # only if used (executor kind min_cpu)
+        return "min" if GPU_API_MODULES.intersection(mods) else "min_cpu"
     return "light"
 
 
 # what the minimal zygote preloads (plus the standard library, imported on
 # demand at stdlib speed)
 MIN_MODULES = frozenset({"numpy", "beekern", "bee_code_interpreter_fs_amd"})
+GPU_API_MODULES = frozenset({"beekern", "bee_code_interpreter_fs_amd"})
 _STDLIB = frozenset(getattr(sys, "stdlib_module_names", ()))
 
 

@@ -50,7 +50,7 @@ void usage() {
           "                    [--timeout S] [--hbm-quota BYTES] [--recursive-scan 0|1] [--preload SO]\n"
           "                    [--pythonpath P] [--max-output BYTES] [--max-idle S] [--acquire-timeout S]\n"
           "                    [--broker-lib SO] [--light-target N] [--light-zygotes N] [--light-preload MODS]\n"
-          "                    [--min-target N] [--min-zygotes N] [--min-preload MODS]\n"
+          "                    [--min-target N] [--min-zygotes N] [--min-preload MODS] [--min-cpu-target N]\n"
           "                    [--workspace DIR] [--runtime-packages DIR] [--die-with-parent 0|1]\n");
 }
 
@@ -123,6 +123,7 @@ int main(int argc, char** argv) {
     else if (a == "--light-preload") cfg.light_preload = val();
     else if (a == "--min-target") cfg.min_target = atoi(val().c_str());
     else if (a == "--min-zygotes") cfg.min_zygotes = atoi(val().c_str());
+    else if (a == "--min-cpu-target") cfg.min_cpu_target = atoi(val().c_str());
     else if (a == "--min-preload") cfg.min_preload = val();
     else if (a == "--runtime-packages") cfg.pod_runtime_packages = val();
     else if (a == "-h" || a == "--help") {

@@ -255,7 +255,7 @@ Zygote* SandboxPool::pick_zygote(int kind) {
   std::vector<Zygote*> same, light;
   for (auto& z : zygotes_) {
     if (!z->alive) continue;
-    if (z->kind == kind) same.push_back(z.get());
+    if (z->kind == kind || (kind == kMinCpu && z->kind == kMin)) same.push_back(z.get());
     if (z->kind == kLight) light.push_back(z.get());
   }
   if (!same.empty()) return same[rr_++ % same.size()];
@@ -448,6 +448,7 @@ std::shared_ptr<Worker> SandboxPool::spawn_worker(bool pooled, int kind, const s
   const bool warm = pooled && kind == kDirect && cfg_.warm_gpu && !gpus.empty();
   env.set("BEE_WARM_GPU", warm ? "1" : "0");
   if (kind != kDirect && broker_) env.set("BEE_BROKER_SOCK", broker_->socket_path());
+  if (kind == kMinCpu) env.set("BEE_BROKER_LAZY", "1");
   if (cfg_.default_hbm_quota > 0) env.set("BEE_HBM_QUOTA_BYTES", std::to_string(cfg_.default_hbm_quota));
   for (auto& kv : extra_env.as_object()) env.set(kv.first, kv.second.is_string() ? kv.second : Json(kv.second.dump()));
 
@@ -490,6 +491,7 @@ void SandboxPool::refill_locked() {
 int SandboxPool::target_of(int kind) const {
   if (kind == kLight) return light_ok_ ? cfg_.light_target : 0;
   if (kind == kMin) return light_ok_ && min_ok_ ? cfg_.min_target : 0;
+  if (kind == kMinCpu) return broker_ && min_ok_ ? (cfg_.min_cpu_target >= 0 ? cfg_.min_cpu_target : cfg_.min_target) : 0;
   return cfg_.target;
 }
 
@@ -777,6 +779,7 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   // its own HIP context (torch & co) or the daemon has no broker
   const std::string mode = req["mode"].str_or(light_ok_ ? "light" : "direct");
   const int kind = !light_ok_ ? kDirect
+                   : mode == "min_cpu" ? (target_of(kMinCpu) > 0 ? kMinCpu : min_ok_ ? kMin : kLight)
                    : mode == "min" ? (min_ok_ ? kMin : kLight)
                    : mode == "light" ? kLight
                                      : kDirect;
@@ -1028,11 +1031,12 @@ Json SandboxPool::status() {
   Json cpu = Json::object();
   for (int i = 0; i < kCpuParts; ++i) cpu.set(kCpuPartNames[i], g_cpu_ns[i].load() / 1e6);
   j.set("cpu_ms", cpu);
-  j.set("ready", (int64_t)(ready_[kDirect].size() + ready_[kLight].size() + ready_[kMin].size()));
+  j.set("ready", (int64_t)(ready_[kDirect].size() + ready_[kLight].size() + ready_[kMin].size() + ready_[kMinCpu].size()));
+  j.set("ready_min_cpu", (int64_t)ready_[kMinCpu].size());
   j.set("ready_min", (int64_t)ready_[kMin].size());
   j.set("ready_direct", (int64_t)ready_[kDirect].size());
   j.set("ready_light", (int64_t)ready_[kLight].size());
-  j.set("spawning", spawning_[kDirect] + spawning_[kLight] + spawning_[kMin]);
+  j.set("spawning", spawning_[kDirect] + spawning_[kLight] + spawning_[kMin] + spawning_[kMinCpu]);
   if (broker_) {
     Json b = Json::object();
     b.set("arch", broker_->arch());
@@ -1082,10 +1086,12 @@ std::string SandboxPool::metrics_text() {
          std::to_string(g_cpu_ns[i].load() / 1e9) + "\n";
   line("bee_executor_inflight", "gauge", (double)m_inflight_.load());
   line("bee_executor_ready_workers", "gauge",
-       (double)(ready_[kDirect].size() + ready_[kLight].size() + ready_[kMin].size()));
+       (double)(ready_[kDirect].size() + ready_[kLight].size() + ready_[kMin].size() + ready_[kMinCpu].size()));
   line("bee_executor_ready_min_workers", "gauge", (double)ready_[kMin].size());
   line("bee_executor_ready_light_workers", "gauge", (double)ready_[kLight].size());
-  line("bee_executor_spawning_workers", "gauge", (double)(spawning_[kDirect] + spawning_[kLight] + spawning_[kMin]));
+  line("bee_executor_ready_min_cpu_workers", "gauge", (double)ready_[kMinCpu].size());
+  line("bee_executor_spawning_workers", "gauge",
+       (double)(spawning_[kDirect] + spawning_[kLight] + spawning_[kMin] + spawning_[kMinCpu]));
   if (broker_) {
     line("bee_executor_broker_ops_total", "counter", (double)broker_->ops());
     line("bee_executor_broker_live_bytes", "gauge", (double)broker_->live_bytes());

@@ -55,6 +55,7 @@ struct PoolConfig {
   std::string light_preload = "numpy,pandas,scipy.stats,matplotlib.pyplot,PIL.Image,bee_code_interpreter_fs_amd.ops";
   int min_target = 0;                  // warm minimal sandboxes kept ready (0 = no minimal zygotes)
   int min_zygotes = 0;                 // parallel forkers for minimal sandboxes
+  int min_cpu_target = -1;             // warm lazy-session minimal sandboxes (-1 = min_target; GPU pools only)
   std::string min_preload = "numpy,bee_code_interpreter_fs_amd.ops";
 };
 
@@ -62,7 +63,10 @@ struct PoolConfig {
 // science stack preloaded.  kMin: broker-backed, only numpy + beekern
 // preloaded -- forks ~5x faster (fork time scales with the zygote's RSS), for
 // scripts that import nothing else.
-enum WorkerKind { kDirect = 0, kLight = 1, kMin = 2, kNumKinds = 3 };
+// kMinCpu: a kMin sandbox whose broker session opens on first use
+// (BEE_BROKER_LAZY=1), for scripts that import no GPU module: they never pay
+// for a session.  Forked by the minimal zygotes.
+enum WorkerKind { kDirect = 0, kLight = 1, kMin = 2, kMinCpu = 3, kNumKinds = 4 };
 
 enum class WorkerState { Spawning, Connected, Ready, Running, Exited, Failed };
 
@@ -171,7 +175,7 @@ class SandboxPool {
   std::map<std::string, std::shared_ptr<Worker>> workers_;  // by id
   std::map<pid_t, std::shared_ptr<Worker>> by_pid_;
   std::deque<std::shared_ptr<Worker>> ready_[kNumKinds];  // by WorkerKind
-  int spawning_[kNumKinds] = {0, 0, 0};
+  int spawning_[kNumKinds] = {0, 0, 0, 0};
   std::unique_ptr<KernelBroker> broker_;
   bool light_ok_ = false;  // light sandboxes available (broker up, or a CPU-only pool)
   bool min_ok_ = false;    // minimal zygotes running

@@ -50,6 +50,25 @@ def test_light_and_direct_sandboxes(gsvc):
     assert direct.stdout.split()[0] == "native", direct.stderr
 
 
+def test_lazy_session_sandbox_can_still_use_the_gpu(gsvc):
+    """A script with no GPU import is routed to a min_cpu sandbox (broker
+    session opened on first use); reaching beekern dynamically still works,
+    and the executor really served it from that pool."""
+    import asyncio
+
+    before = asyncio.run_coroutine_threadsafe(gsvc.ctx.code_executor.status(), gsvc.loop).result(30)
+    code = (
+        "import importlib, os\n"
+        "print(os.environ.get('BEE_BROKER_LAZY'))\n"
+        "bk = importlib.import_module('bee' + 'kern')\n"
+        "print(round(float(bk.sum(bk.square(bk.random.rand(1 << 20)))) / (1 << 20), 2), bk.driver_name())\n"
+    )
+    r = run(gsvc, code)
+    assert r.exit_code == 0, r.stderr
+    assert r.stdout.split() == ["1", "0.33", "broker"], r.stdout
+    assert before["slots"][0]["executor"].get("min_target", 0) > 0
+
+
 def test_broker_rejects_out_of_bounds(gsvc):
     code = (
         "from bee_code_interpreter_fs_amd.ops.array import driver\n"
