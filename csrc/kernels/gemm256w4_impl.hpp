@@ -62,6 +62,14 @@ enum : int {
   kInterleave = 2,  // sched_group_barrier: spread ds_read / glds among the MFMAs
   kNoCarry = 4,     // no fragment prefetch across the barrier: both k-halves read at the top of the iteration
   kDirectStore = 8, // epilogue: each lane stores its accumulators straight to C (no LDS staging)
+  // MFMAs as inline asm with AGPR-constrained accumulators ("+a"): the 256
+  // accumulator registers are pinned in the AGPR file, so the allocator has
+  // nothing to shuffle (the builtin form got v_accvgpr_read/write copies in
+  // the loop, tools/gemm_lab/isa_check.sh).  The hazard recognizer does not
+  // see through inline asm, so accumulator reads after the loop are fenced by
+  // explicit wait states (mfma_drain).
+  kAsmMfma = 16,
+  kEarlyGlds = 32,  // kAsmMfma|kInterleave: all K-tile loads in the first 8 of the second k-half's 16 groups
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
@@ -133,11 +141,25 @@ __device__ __forceinline__ void read_frags(const uint16_t* buf, int wr, int wc, 
   for (int j = 0; j < 8; ++j) fb[j] = frag(buf + kOperand, wc * 128 + j * 16 + (lane & 15), s * 4 + (lane >> 4));
 }
 
+template <bool ASM = false>
 __device__ __forceinline__ void mfma_block(f32x4 (&acc)[8][8], const bf16x8 (&fa)[8], const bf16x8 (&fb)[8]) {
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (ASM)
+        asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fa[i]), "v"(fb[j]));
+      else
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+}
+
+// wait states between the last inline-asm MFMA and any read of its result
+// (16x16x32 bf16: 8 passes; 3 x s_nop 7 = 24 wait states covers it)
+__device__ __forceinline__ void mfma_drain() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // 64 MFMAs with `ds` ds_reads and `vm` VMEM ops spread evenly among them
@@ -149,6 +171,72 @@ __device__ __forceinline__ void interleave_hint() {
     if constexpr (VM > 0) __builtin_amdgcn_sched_group_barrier(0x020, VM / slots, 0);
     if constexpr (DS > 0) __builtin_amdgcn_sched_group_barrier(0x100, DS / slots, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+  }
+}
+
+// one MFMA as inline asm; INIT: C starts from the constant 0
+template <bool INIT>
+__device__ __forceinline__ void mfma_asm(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  if constexpr (INIT)
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+  else
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// the i-th of one operand's 8 K-tile glds (stage() split up)
+__device__ __forceinline__ void glds_one(const Panel& p, int k0, uint16_t* lds_operand, int wave, int i) {
+  const int soff = (wave * 64 + i * 8) * p.row_bytes + k0 * 2;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(p.rsrc, (lds_void_ptr)(lds_operand + (wave * kGlds + i) * 8 * TK), 16,
+                                           p.lane_off[i & 1], soff, 0, 0);
+}
+
+// One K-tile of the kAsmMfma|kInterleave schedule, in 2 x 16 groups fenced by
+// sched_barrier(0) so the issue order is exactly this:
+//   k-half 0: [4 MFMA(fa0,fb0) + ds_read of one fa1/fb1 fragment] x 16
+//   s_waitcnt(0); s_barrier
+//   k-half 1: [4 MFMA(fa1,fb1) + one glds of tile t+2 + ds_read of one
+//              fa0/fb0 fragment of tile t+1] x 16
+// A ds_read overwrites a fragment register >= 16 MFMAs after its last reader
+// (WAR on srcA/B of an in-flight MFMA, invisible to the hazard recognizer
+// through inline asm).
+template <bool INIT, bool EARLY>
+__device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8], bf16x8 (&fa1)[8],
+                                          bf16x8 (&fb1)[8], uint16_t* smem, const Panel& pa, const Panel& pb, int t,
+                                          int nk, int wr, int wc, int lane, int wave) {
+  uint16_t* cur = smem + (t & 1) * kBuf;
+  uint16_t* nxt = smem + ((t & 1) ^ 1) * kBuf;
+  const int rl = lane & 15, ch = lane >> 4;
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) mfma_asm<INIT>(acc[g >> 1][(g & 1) * 4 + jj], fa0[g >> 1], fb0[(g & 1) * 4 + jj]);
+    if (g < 8) fa1[g] = frag(cur, wr * 128 + g * 16 + rl, 4 + ch);
+    else fb1[g - 8] = frag(cur + kOperand, wc * 128 + (g - 8) * 16 + rl, 4 + ch);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  barrier();
+  const int kn = min(t + 2, nk - 1) * TK;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) mfma_asm<false>(acc[g >> 1][(g & 1) * 4 + jj], fa1[g >> 1], fb1[(g & 1) * 4 + jj]);
+    if constexpr (EARLY) {  // all 16 glds in the first 8 groups: more time to land
+      if (g < 8) {
+        glds_one(pa, kn, cur, wave, g);
+        glds_one(pb, kn, cur + kOperand, wave, g);
+      }
+    } else {
+      if (g < 8) glds_one(pa, kn, cur, wave, g);
+      else glds_one(pb, kn, cur + kOperand, wave, g - 8);
+    }
+    // in the order the next K-tile's first groups consume them: fa0[0],
+    // fb0[0..7], fa0[1..7]
+    if (g == 0) fa0[0] = frag(nxt, wr * 128 + rl, ch);
+    else if (g <= 8) fb0[g - 1] = frag(nxt + kOperand, wc * 128 + (g - 1) * 16 + rl, ch);
+    else fa0[g - 8] = frag(nxt, wr * 128 + (g - 8) * 16 + rl, ch);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -210,7 +298,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
                                                                   void* __restrict__ C, int M, int N, int K, int lda,
                                                                   int ldb, int ldc, float alpha, float beta) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[kSmemBytes / 2];  // the only LDS object
-  constexpr bool pin = (O & kPinOrder) != 0, inter = (O & kInterleave) != 0;
+  constexpr bool pin = (O & kPinOrder) != 0, inter = (O & kInterleave) != 0, am = (O & kAsmMfma) != 0,
+                 early = (O & kEarlyGlds) != 0;
 
   const int nbm = M / TM, nbn = N / TN, nblocks = nbm * nbn;
   const int b = xcd_remap(blockIdx.x, nblocks);
@@ -246,15 +335,21 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   barrier();
 
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
-  if constexpr ((O & kNoCarry) != 0) {
+  if constexpr (am && inter) {
+    // hand-interleaved pipeline; K-tile 0 peeled so its MFMAs start the
+    // accumulators from the constant 0 (no AGPR zero-fill to fence)
+    read_frags(smem, wr, wc, lane, 0, fa0, fb0);
+    ktile_asm<true, early>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
+    for (int t = 1; t < nk; ++t) ktile_asm<false, early>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
+  } else if constexpr ((O & kNoCarry) != 0) {
     // loop-carried state is the accumulators only (simpler register
     // allocation); the first MFMAs of each K-tile wait for its first reads
     for (int t = 0; t < nk; ++t) {
       uint16_t* cur = smem + (t & 1) * kBuf;
       read_frags(cur, wr, wc, lane, 0, fa0, fb0);
       read_frags(cur, wr, wc, lane, 1, fa1, fb1);
-      mfma_block(acc, fa0, fb0);
-      mfma_block(acc, fa1, fb1);
+      mfma_block<am>(acc, fa0, fb0);
+      mfma_block<am>(acc, fa1, fb1);
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       barrier();
       const int kn = min(t + 2, nk - 1) * TK;
@@ -270,7 +365,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
     read_frags(cur, wr, wc, lane, 1, fa1, fb1);
     if constexpr (inter) interleave_hint<16, 0>();
     else if constexpr (pin) __builtin_amdgcn_sched_barrier(0);
-    mfma_block(acc, fa0, fb0);
+    mfma_block<am>(acc, fa0, fb0);
     if constexpr (pin || inter) __builtin_amdgcn_sched_barrier(0);
 
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -285,7 +380,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
     read_frags(nxt, wr, wc, lane, 0, fa0, fb0);
     if constexpr (inter) interleave_hint<16, 16>();
     else if constexpr (pin) __builtin_amdgcn_sched_barrier(0);
-    mfma_block(acc, fa1, fb1);
+    mfma_block<am>(acc, fa1, fb1);
     if constexpr (pin || inter) __builtin_amdgcn_sched_barrier(0);
   }
   }
@@ -294,6 +389,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   // staging writes
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   barrier();
+  if constexpr (am) mfma_drain();
   if constexpr ((O & kDirectStore) != 0) {
     // 16x16 C/D map: lane holds rows 4*(lane/16)+r of column lane%16 -> 4
     // scattered element stores per fragment (f32 output only; cheap on

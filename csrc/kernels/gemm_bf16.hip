@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256) void transpose_bf16(const uint16_t* __restrict
 
 bool gemm256_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16);  // gemm_bf16_256.hip
 void launch_gemm256(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
-                    float beta, bool out_bf16, hipStream_t stream);
+                    float beta, bool out_bf16, hipStream_t stream, int which);
 
 }  // namespace bk
 
@@ -261,7 +261,8 @@ BK_API int bk_gemm_bf16_fast_ok(int M, int N, int K, int lda, int ldb) {
 // Kernel choice: the 256x256 phase-pipelined kernel when the shape fills at
 // least half the chip with 256^2 tiles, the 128x128 kernel for smaller
 // aligned shapes (4x the blocks), the guarded generic kernel otherwise.
-// variant: 0 = auto, 1 = generic, 2 = 128x128, 3 = 256x256 (benchmarks).
+// variant: 0 = auto, 1 = generic, 2 = 128x128, 3 = 256x256 (4-wave or 8-wave
+// by K), 4 = 256x256 8-wave, 5 = 256x256 4-wave (benchmarks, tests).
 BK_API int bk_gemm_bf16_tn_variant(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb,
                                    int ldc, float alpha, float beta, int out_dtype, int variant, hipStream_t stream) {
   if (!A || !Bt || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N) return kBadArgument;
@@ -270,10 +271,11 @@ BK_API int bk_gemm_bf16_tn_variant(const void* A, const void* Bt, void* C, int M
   const bool ok128 = al && bk_gemm_bf16_fast_ok(M, N, K, lda, ldb);
   const bool ok256 = al && aligned16(C) && gemm256_ok(M, N, K, lda, ldb, ldc, out_dtype == kBF16);
   if (variant == 0) variant = (ok256 && (M / 256) * (N / 256) >= 128) ? 3 : ok128 ? 2 : 1;
-  if ((variant == 3 && !ok256) || (variant == 2 && !ok128)) return kBadArgument;
+  if ((variant >= 3 && variant <= 5 && !ok256) || (variant == 2 && !ok128) || variant < 1 || variant > 5)
+    return kBadArgument;
   const bool bf = out_dtype == kBF16;
-  if (variant == 3) {
-    launch_gemm256(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, bf, stream);
+  if (variant >= 3) {
+    launch_gemm256(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, bf, stream, variant - 3);
   } else if (variant == 2) {
     const unsigned grid = (unsigned)((M / BM) * (N / BN));
     if (bf)

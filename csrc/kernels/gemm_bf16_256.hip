@@ -1,20 +1,33 @@
-// Shipped instantiation of the 256x256 phase-pipelined bf16 GEMM
-// (gemm256_impl.hpp holds the kernel and the schedule notes).  The schedule
-// chosen here is the winner of tools/gemm_lab.py on MI355X
-// (profiles/r1_gemm_lab.log).
+// Shipped instantiations of the 256x256 bf16 GEMMs:
+//   * the 8-wave phase-pipelined kernel (gemm256_impl.hpp, 128x64 per wave)
+//   * the 4-wave kernel (gemm256w4_impl.hpp, 128x128 per wave) with inline-asm
+//     MFMAs on AGPR accumulators and a hand-interleaved load/MFMA schedule
+// Both schedules are winners of tools/gemm_lab.py on MI355X
+// (profiles/r1_gemm_lab.log): the 4-wave kernel issues half the LDS reads per
+// MFMA and wins from K >= 256 on (4096^3: 1401 vs 1259 TFLOP/s); the 8-wave
+// kernel wins short-K shapes, where the 4-wave prologue/epilogue dominate.
 #include "gemm256_impl.hpp"
+#include "gemm256w4_impl.hpp"
 
 namespace bk {
 
 constexpr int kShipped = g256::kOptRound1;
+constexpr int kShippedW4 = g4::kAsmMfma | g4::kInterleave;
+constexpr int kW4MinK = 256;
 
 bool gemm256_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16) {
   return g256::ok(M, N, K, lda, ldb, ldc, out_bf16);
 }
 
+// which: 0 = by shape, 1 = 8-wave, 2 = 4-wave
 void launch_gemm256(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
-                    float beta, bool out_bf16, hipStream_t stream) {
-  g256::launch<kShipped>(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, out_bf16, stream);
+                    float beta, bool out_bf16, hipStream_t stream, int which) {
+  const bool w4_ok = g4::ok(M, N, K, lda, ldb, ldc, out_bf16);
+  if (which == 0) which = (w4_ok && K >= kW4MinK) ? 2 : 1;
+  if (which == 2 && w4_ok)
+    g4::launch<kShippedW4>(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, out_bf16, stream);
+  else
+    g256::launch<kShipped>(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, out_bf16, stream);
 }
 
 }  // namespace bk

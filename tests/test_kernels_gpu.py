@@ -218,11 +218,12 @@ def test_torch_interop(gpu):
     torch.testing.assert_close(back, t * t)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("out", ["float32", "bfloat16"])
 def test_gemm_kernel_variants_with_beta(gpu, variant, out):
-    """Every GEMM kernel (generic / 128^2 / 256^2 phase-pipelined) against an
-    fp64 reference, including the beta * C read-modify-write epilogue."""
+    """Every GEMM kernel (generic / 128^2 / 256^2 by shape / 256^2 8-wave
+    phase-pipelined / 256^2 4-wave inline-asm MFMA) against an fp64
+    reference, including the beta * C read-modify-write epilogue."""
     import torch
 
     from bee_code_interpreter_fs_amd.ops import _native
