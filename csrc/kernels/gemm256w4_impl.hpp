@@ -31,6 +31,11 @@
 // so the MFMA stream only stops at the barrier, every LDS read has 64 MFMAs
 // (>= 1024 cycles) to land, and every K-tile load has one whole iteration.
 // The only vmcnt(0) in the loop waits for loads issued an iteration earlier.
+//
+// Shipped options (gemm_bf16_256.hip): kAsmMfma | kInterleave = the same
+// loop with inline-asm MFMAs and an explicit issue order (ktile_asm below);
+// with builtin MFMAs the allocator moved accumulators through v_accvgpr_mov
+// in the loop and the kernel lost to the 8-wave one.
 #pragma once
 #include "bk_common.hpp"
 
