@@ -290,11 +290,12 @@ def _prefault() -> None:
         doc = json.loads(json.dumps({"op": "run", "script": "/x", "argv": [], "env": {"A": "1"}}))
         code = compile("import sys\nx = [i * i for i in range(64)]\n", "<prefault>", "exec", dont_inherit=True)
         exec(code, {"__builtins__": builtins, "__name__": "__prefault__"})
-        os.environ["BEE_PREFAULT"] = doc["env"]["A"]
-        del os.environ["BEE_PREFAULT"]
+        os.environ["BEE_PREFAULT_SCRATCH"] = doc["env"]["A"]
+        del os.environ["BEE_PREFAULT_SCRATCH"]
         _to_logical("/a/b", "/a", "/workspace")
         io.TextIOWrapper(io.BufferedWriter(io.FileIO(os.open(os.devnull, os.O_WRONLY), "w")), encoding="utf-8").close()
-        traceback.TracebackException(ValueError, ValueError("x"), None).format()
+        if os.environ.get("BEE_PREFAULT_TB") == "1":
+            traceback.TracebackException(ValueError, ValueError("x"), None).format()
     except Exception:
         pass
 
@@ -356,7 +357,8 @@ def worker_main(spawn: dict) -> None:
         warm = os.environ.get("BEE_WARM_GPU") == "1" or bool(os.environ.get("BEE_BROKER_SOCK"))
         gpu_error = warm_gpu() if warm else None
         _cpu_stamp("warm")
-        _prefault()
+        if os.environ.get("BEE_PREFAULT", "1") != "0":
+            _prefault()
         _prefault_scientific()
         _cpu_stamp("prefault")
         _send(sock, {"op": "ready", "warm_ms": (time.perf_counter() - t0) * 1e3, "gpu_error": gpu_error or ""})

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--n", type=int, default=200)
     ap.add_argument("--payload", default=os.path.join(ROOT, "examples", "hello_world.py"))
     ap.add_argument("--preload", default="numpy,bee_code_interpreter_fs_amd.ops")
+    ap.add_argument("--no-prefault", action="store_true", help="skip worker._prefault (A/B of its net CPU)")
     args = ap.parse_args()
     os.environ["BEE_PRELOAD"] = args.preload
     os.environ["BEE_ZYGOTE_KIND"] = "light"
@@ -45,7 +46,7 @@ def main():
     with open(script, "w") as fh:
         fh.write(open(args.payload).read())
     phases = {}
-    teardown, parent_fork, wall = [], [], []
+    teardown, parent_fork, wall, tot = [], [], [], []
     r_fd, w_fd = os.pipe()
     for _ in range(args.n):
         p0 = cpu()[0]
@@ -59,7 +60,8 @@ def main():
             os.chdir(work)
             worker._apply_limits()
             marks.append(("setup", *cpu()))
-            worker._prefault()
+            if not args.no_prefault:
+                worker._prefault()
             marks.append(("prefault", *cpu()))
             worker._redirect_stdio(os.path.join(work, "o.txt"), os.path.join(work, "e.txt"))
             marks.append(("redirect", *cpu()))
@@ -83,12 +85,14 @@ def main():
             prev_c, prev_f = c, f
         total_child = (ru.ru_utime + ru.ru_stime) * 1e3
         teardown.append(total_child - marks[-1][1])
+        tot.append(total_child)
     out = {"preload": args.preload, "zygote_rss_mb": round(rss, 1), "n": args.n,
            "parent_fork_cpu_ms": round(statistics.median(parent_fork), 3),
            "child_start_cpu_ms": None,
            "phases_cpu_ms": {k: round(statistics.median(c for c, _ in v), 3) for k, v in phases.items()},
            "phases_minflt": {k: statistics.median(f for _, f in v) for k, v in phases.items()},
            "teardown_cpu_ms": round(statistics.median(teardown), 3),
+           "child_total_cpu_ms": round(statistics.median(tot), 3),
            "wall_ms": round(statistics.median(wall), 3)}
     print(json.dumps(out))
 
