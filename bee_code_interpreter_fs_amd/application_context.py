@@ -9,6 +9,8 @@ initial pool fill, `:83`, dropping its exceptions).
 
 from __future__ import annotations
 
+import asyncio
+import contextlib
 import logging
 import os
 from functools import cached_property
@@ -98,6 +100,27 @@ class ApplicationContext:
 
     async def start(self) -> None:
         await self.code_executor.start()
+        ttl = float(self.config.file_storage_ttl_seconds or 0)
+        if ttl > 0:
+            self._sweeper = asyncio.create_task(self._sweep_storage(ttl))
+
+    async def _sweep_storage(self, ttl: float) -> None:
+        """Object retention (``APP_FILE_STORAGE_TTL_SECONDS``):
+        sweep a quarter-TTL apart (1 s .. 5 min), off the event loop."""
+        period = min(max(ttl / 4, 1.0), 300.0)
+        while True:
+            try:
+                n = await asyncio.to_thread(self.file_storage.sweep, ttl)
+                if n:
+                    logger.info("storage sweep removed %d object(s) older than %.0f s", n, ttl)
+            except Exception:  # keep sweeping; a failed pass is logged, not fatal
+                logger.exception("storage sweep failed")
+            await asyncio.sleep(period)
 
     async def close(self) -> None:
+        task = self.__dict__.pop("_sweeper", None)
+        if task is not None:
+            task.cancel()
+            with contextlib.suppress(asyncio.CancelledError):
+                await task
         await self.code_executor.close()

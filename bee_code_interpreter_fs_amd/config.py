@@ -72,6 +72,9 @@ class Config:
     executor_pod_spec_extra: Dict[str, Any] = field(default_factory=dict)
     # directory of the file-object store
     file_storage_path: str = "./.tmp/files"
+    # delete stored objects older than this many seconds (0 = keep forever,
+    # the reference's behaviour)
+    file_storage_ttl_seconds: float = 0.0
     # how many executor pods (kubernetes) to keep ready for immediate use
     executor_pod_queue_target_length: int = 5
     # prefix of executor pod names; 6 random [a-z0-9] follow

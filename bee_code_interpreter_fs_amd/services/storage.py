@@ -21,6 +21,7 @@ from __future__ import annotations
 import contextlib
 import os
 import secrets
+import time
 from typing import AsyncIterator, Optional
 
 import anyio
@@ -158,6 +159,35 @@ class Storage:
             os.unlink(path)
         except (ValueError, FileNotFoundError, IsADirectoryError):
             raise FileNotFoundError(f"File not found: {object_id}")
+
+    # -- retention -----------------------------------------------------------
+    def sweep(self, max_age_s: float, now: Optional[float] = None) -> int:
+        """Delete objects (and abandoned temp files) stored more than
+        ``max_age_s`` seconds ago; returns how many were removed.
+
+        The reference leaves retention to operators ("clean old objects
+        periodically", `README.md:61`); ``APP_FILE_STORAGE_TTL_SECONDS`` runs
+        this from the service.  Age is measured from the inode change time:
+        ``rename`` (written objects) and ``link`` (adopted sandbox files) both
+        set it, so an adopted file's own older mtime does not count."""
+        now = time.time() if now is None else now
+        removed = 0
+        for d in (self.storage_path, self._tmp):
+            try:
+                entries = list(os.scandir(d))
+            except FileNotFoundError:
+                continue
+            for e in entries:
+                try:
+                    if not e.is_file(follow_symlinks=False):
+                        continue
+                    st = e.stat(follow_symlinks=False)
+                    if now - max(st.st_ctime, st.st_mtime) > max_age_s:
+                        os.unlink(e.path)
+                        removed += 1
+                except FileNotFoundError:
+                    continue  # deleted concurrently (another replica's sweep, a DELETE)
+        return removed
 
 
 def _copy_file(src: str, dst: str) -> None:
