@@ -63,7 +63,7 @@ def _targets() -> List[Target]:
             compiler=HIPCC,
             compile_flags=HIP_FLAGS,
             link_flags=[f"--offload-arch={ARCH}", "-shared", "-fPIC"],
-            headers=[os.path.join(k, "bk_common.hpp"), os.path.join(k, "bk_philox.hpp"), os.path.join(k, "gemm256_impl.hpp")],
+            headers=[os.path.join(k, f) for f in ("bk_common.hpp", "bk_philox.hpp", "gemm256_impl.hpp", "gemm256w4_impl.hpp")],
             hip=True,
         ),
     ]
@@ -78,7 +78,8 @@ def _targets() -> List[Target]:
                     "-O2", "-g", "-std=c++17", "-Wall", "-Wextra", "-Wno-unused-parameter", "-Wno-unused-result",
                     "-pthread", f"-I{ROCM}/include", "-D__HIP_PLATFORM_AMD__",
                 ],
-                link_flags=["-pthread", f"-L{ROCM}/lib", "-lamdhip64", "-ldl", f"-Wl,-rpath,{ROCM}/lib"],
+                link_flags=["-pthread", f"-L{ROCM}/lib", "-lamdhip64", "-lrocprofiler-sdk-roctx", "-ldl",
+                            f"-Wl,-rpath,{ROCM}/lib"],
                 shared=False,
                 headers=sorted(os.path.join(ex, f) for f in os.listdir(ex) if f.endswith(".hpp")),
             )
@@ -109,7 +110,8 @@ def _targets() -> List[Target]:
                     compiler=CXX,
                     compile_flags=["-O1", "-g", "-std=c++17", "-pthread", f"-I{ROCM}/include",
                                    "-D__HIP_PLATFORM_AMD__", *flags, *extra],
-                    link_flags=[*flags, "-pthread", f"-L{ROCM}/lib", "-lamdhip64", "-ldl", f"-Wl,-rpath,{ROCM}/lib"],
+                    link_flags=[*flags, "-pthread", f"-L{ROCM}/lib", "-lamdhip64", "-lrocprofiler-sdk-roctx", "-ldl",
+                                f"-Wl,-rpath,{ROCM}/lib"],
                     shared=False,
                     headers=ex_hdrs,
                     optional=True,

@@ -3,6 +3,7 @@
 #include <dlfcn.h>
 #include <errno.h>
 #include <hip/hip_runtime_api.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
@@ -30,6 +31,22 @@ enum Status : int32_t {
   kBadHandle = 6, kProtocol = 7,
 };
 constexpr uint64_t kMaxFrame = 1ull << 30;
+
+// roctx range names per op: `rocprofv3 --marker-trace --kernel-trace` of the
+// daemon shows which sandbox request each broker kernel belongs to (ranges
+// cost a table lookup when no profiler is attached)
+const char* op_name(uint32_t op) {
+  static const char* const names[] = {"bk.?",      "bk.hello", "bk.alloc", "bk.free",      "bk.write",
+                                      "bk.read",   "bk.rand",  "bk.unary", "bk.binary",    "bk.cast",
+                                      "bk.fill",   "bk.reduce", "bk.gemm", "bk.transpose", "bk.sync",
+                                      "bk.memstats", "bk.info", "bk.copy", "bk.rand_reduce"};
+  return op < sizeof(names) / sizeof(names[0]) ? names[op] : names[0];
+}
+
+struct RoctxRange {
+  explicit RoctxRange(const char* name) { roctxRangePushA(name); }
+  ~RoctxRange() { roctxRangePop(); }
+};
 constexpr uint32_t kNoReply = 1;  // request flag
 
 int dsize(int dt) {
@@ -304,6 +321,7 @@ void KernelBroker::serve(int fd, pid_t peer) {
     payload.resize(len);
     if (len && !read_exact(fd, payload.data(), len)) break;
     CpuScope cpu(kCpuBroker);
+    RoctxRange range(op_name(op));
     Reader r{payload.data(), payload.size()};
     out.clear();
     int32_t st = kOk;

@@ -9,7 +9,7 @@ D=$(mktemp -d /tmp/bee-prof-XXXXXX)
 mkdir -p gpurun_out
 mapfile -t CMD < <(python tools/prof_served.py cmd "$D")
 export BEE_PROFILE_DAEMON_ONLY=1 TMPDIR=/tmp
-timeout -k 10 150 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_served -o run -- "${CMD[@]}" \
+timeout -k 10 150 rocprofv3 --kernel-trace --marker-trace --stats -d gpurun_out/prof_served -o run -- "${CMD[@]}" \
   > gpurun_out/prof_served_daemon.log 2>&1 &
 ROC=$!
 timeout -k 10 180 python tools/prof_served.py drive "$D" --n "$N"
