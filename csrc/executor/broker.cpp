@@ -185,6 +185,16 @@ bool KernelBroker::start(std::string* err) {
     return false;
   }
   g_bk.set_quota(0);  // quotas are enforced per connection here
+  {
+    // load every kernel module now, not on a sandbox's first request
+    int (*preload)(hipStream_t) = nullptr;
+    if (sym(lib_, "bk_preload", &preload)) {
+      const double tp = mono_ms();
+      const int rc = preload(nullptr);
+      if (rc != 0) BEE_WARN("bk_preload failed (%d): %s", rc, g_bk.last_error());
+      else BEE_INFO("kernel broker: kernel modules loaded in %.0f ms", mono_ms() - tp);
+    }
+  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, 0) == hipSuccess) arch_ = prop.gcnArchName;
   BEE_INFO("kernel broker: HIP context on %s ready in %.0f ms", arch_.c_str(), mono_ms() - t0);

@@ -1,6 +1,7 @@
 """Summarise a rocprofv3 SQLite output (rocpd schema) into small CSVs for
 profiles/: per-kernel call count / mean / min duration, and per-kernel mean
-PMC counter values when counters were collected.
+PMC counter values when counters were collected, and per-range call count /
+mean duration of roctx ranges when markers were traced (--marker-trace).
 
     python tools/rocpd_summary.py gpurun_out/prof/xxx_results.db profiles/name
 """
@@ -39,7 +40,20 @@ def main():
             w.writerow(["kernel", "counter", "mean_value", "dispatches"])
             for name, c, v, n in pm:
                 w.writerow([short(name), c, v, n])
-    print(f"{len(rows)} kernels, {len(pm)} counter rows -> {prefix}_*.csv")
+    # roctx ranges (--marker-trace): the kernel broker's per-op ranges
+    try:
+        rg = list(cur.execute(
+            "select json_extract(extdata, '$.message') as m, count(*), avg(end - start), min(end - start), "
+            "sum(end - start) from regions where category like 'MARKER%' group by m order by sum(end - start) desc"))
+    except sqlite3.Error:
+        rg = []
+    if rg:
+        with open(prefix + "_ranges.csv", "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["range", "calls", "mean_us", "min_us", "total_ms"])
+            for m, n, avg, mn, tot in rg:
+                w.writerow([m, n, round(avg / 1e3, 2), round(mn / 1e3, 2), round(tot / 1e6, 2)])
+    print(f"{len(rows)} kernels, {len(pm)} counter rows, {len(rg)} ranges -> {prefix}_*.csv")
 
 
 if __name__ == "__main__":
