@@ -84,6 +84,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "bk_memcpy": ([c_vp, c_vp, c_i64, c_int, c_vp], c_int),
         "bk_memcpy_async": ([c_vp, c_vp, c_i64, c_int, c_vp], c_int),
         "bk_sync": ([c_vp], c_int),
+        "bk_preload": ([c_vp], c_int),
         "bk_device_info": ([ctypes.POINTER(c_i64), ctypes.c_char_p, c_int], c_int),
         "bk_event_pair_create": ([ctypes.POINTER(c_vp), ctypes.POINTER(c_vp)], c_int),
         "bk_event_record": ([c_vp, c_vp], c_int),

@@ -246,6 +246,18 @@ def test_gemm_kernel_variants_with_beta(gpu, variant, out):
     assert (c.double() - ref).abs().max().item() < tol * max(1.0, ref.abs().max().item())
 
 
+def test_preload_loads_every_kernel_module(gpu):
+    """bk_preload (called by the kernel broker at startup) runs one tiny
+    launch per kernel module and frees what it allocated."""
+    import torch
+
+    from bee_code_interpreter_fs_amd.ops import _native
+
+    before = gpu.memory_stats()["in_use"]
+    assert _native.lib().bk_preload(torch.cuda.current_stream().cuda_stream) == 0
+    assert gpu.memory_stats()["in_use"] == before
+
+
 @pytest.mark.parametrize("dtype", ["float64", "float32"])
 @pytest.mark.parametrize("n", [1, 3, 1001, 1 << 20, 10**7 + 3])
 def test_fused_rand_reduce_matches_materialised(gpu, dtype, n):
