@@ -74,7 +74,8 @@ enum : int {
   // see through inline asm, so accumulator reads after the loop are fenced by
   // explicit wait states (mfma_drain).
   kAsmMfma = 16,
-  kEarlyGlds = 32,  // kAsmMfma|kInterleave: all K-tile loads in the first 8 of the second k-half's 16 groups
+  kEarlyGlds = 32,   // kAsmMfma|kInterleave: all K-tile loads in the first 8 of the second k-half's 16 groups
+  kReadsEarly = 64,  // kAsmMfma|kInterleave: k-half-1 fragment reads done by group 11 of 16
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
@@ -204,7 +205,7 @@ __device__ __forceinline__ void glds_one(const Panel& p, int k0, uint16_t* lds_o
 // A ds_read overwrites a fragment register >= 16 MFMAs after its last reader
 // (WAR on srcA/B of an in-flight MFMA, invisible to the hazard recognizer
 // through inline asm).
-template <bool INIT, bool EARLY>
+template <bool INIT, bool EARLY, bool READS_EARLY>
 __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8], bf16x8 (&fa1)[8],
                                           bf16x8 (&fb1)[8], uint16_t* smem, const Panel& pa, const Panel& pb, int t,
                                           int nk, int wr, int wc, int lane, int wave) {
@@ -216,8 +217,22 @@ __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], 
   for (int g = 0; g < 16; ++g) {
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) mfma_asm<INIT>(acc[g >> 1][(g & 1) * 4 + jj], fa0[g >> 1], fb0[(g & 1) * 4 + jj]);
-    if (g < 8) fa1[g] = frag(cur, wr * 128 + g * 16 + rl, 4 + ch);
-    else fb1[g - 8] = frag(cur + kOperand, wc * 128 + (g - 8) * 16 + rl, 4 + ch);
+    auto read1 = [&](int i) {  // i-th of the 16 k-half-1 fragments: fa1[0..7], fb1[0..7]
+      if (i < 8) fa1[i] = frag(cur, wr * 128 + i * 16 + rl, 4 + ch);
+      else fb1[i - 8] = frag(cur + kOperand, wc * 128 + (i - 8) * 16 + rl, 4 + ch);
+    };
+    if constexpr (READS_EARLY) {
+      // all 16 reads by group 11 (2 per group in 0..3): the lgkmcnt(0) before
+      // the barrier then has 16 MFMAs to cover the last read's latency
+      if (g < 4) {
+        read1(2 * g);
+        read1(2 * g + 1);
+      } else if (g < 12) {
+        read1(g + 4);
+      }
+    } else {
+      read1(g);
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -304,7 +319,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
                                                                   int ldb, int ldc, float alpha, float beta) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[kSmemBytes / 2];  // the only LDS object
   constexpr bool pin = (O & kPinOrder) != 0, inter = (O & kInterleave) != 0, am = (O & kAsmMfma) != 0,
-                 early = (O & kEarlyGlds) != 0;
+                 early = (O & kEarlyGlds) != 0, reads_early = (O & kReadsEarly) != 0;
 
   const int nbm = M / TM, nbn = N / TN, nblocks = nbm * nbn;
   const int b = xcd_remap(blockIdx.x, nblocks);
@@ -344,8 +359,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
     // hand-interleaved pipeline; K-tile 0 peeled so its MFMAs start the
     // accumulators from the constant 0 (no AGPR zero-fill to fence)
     read_frags(smem, wr, wc, lane, 0, fa0, fb0);
-    ktile_asm<true, early>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
-    for (int t = 1; t < nk; ++t) ktile_asm<false, early>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
+    ktile_asm<true, early, reads_early>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
+    for (int t = 1; t < nk; ++t) ktile_asm<false, early, reads_early>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
   } else if constexpr ((O & kNoCarry) != 0) {
     // loop-carried state is the accumulators only (simpler register
     // allocation); the first MFMAs of each K-tile wait for its first reads

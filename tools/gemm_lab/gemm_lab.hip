@@ -25,7 +25,9 @@ void run(const void* A, const void* B, void* C, int M, int N, int K, int lda, in
 // 4-wave 128x128-per-wave kernel options, lab ids 6..
 constexpr int kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave, g4::kNoCarry, g4::kDirectStore,
                            g4::kAsmMfma | g4::kInterleave, g4::kAsmMfma | g4::kNoCarry,
-                           g4::kAsmMfma | g4::kInterleave | g4::kEarlyGlds};
+                           g4::kAsmMfma | g4::kInterleave | g4::kEarlyGlds,
+                           g4::kAsmMfma | g4::kInterleave | g4::kReadsEarly,
+                           g4::kAsmMfma | g4::kInterleave | g4::kReadsEarly | g4::kEarlyGlds};
 template <int I>
 void run_w4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool bf,
             hipStream_t s) {
@@ -53,6 +55,8 @@ BK_API int gemmlab_run(int variant, const void* A, const void* Bt, void* C, int 
     case 11: run_w4<5>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 12: run_w4<6>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 13: run_w4<7>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 14: run_w4<8>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 15: run_w4<9>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     default: return kBadArgument;
   }
   return launch_status();
