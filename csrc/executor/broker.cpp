@@ -277,6 +277,32 @@ void give_stream(hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_stream_mu);
   g_streams.push_back(s);
 }
+
+// Reduction results land in pinned, host-coherent memory: the final reduce
+// stage writes the scalar straight to the host, so a reduce costs one stream
+// sync instead of a D2H copy (a staging blit kernel + copy bookkeeping, 2 per
+// headline Execute) plus the sync.  One 64-byte slot per connection, carved
+// from 4 KiB pinned pages and recycled like the streams.
+std::mutex g_slot_mu;
+std::vector<double*> g_slots;
+
+double* take_slot() {
+  std::lock_guard<std::mutex> lk(g_slot_mu);
+  if (g_slots.empty()) {
+    void* page = nullptr;
+    if (hipHostMalloc(&page, 4096, hipHostMallocCoherent) != hipSuccess || page == nullptr) return nullptr;
+    for (int i = 0; i < 4096 / 64; ++i) g_slots.push_back((double*)((char*)page + i * 64));
+  }
+  double* s = g_slots.back();
+  g_slots.pop_back();
+  return s;
+}
+
+void give_slot(double* s) {
+  if (s == nullptr) return;
+  std::lock_guard<std::mutex> lk(g_slot_mu);
+  g_slots.push_back(s);
+}
 }  // namespace
 
 void KernelBroker::serve(int fd, pid_t peer) {
@@ -288,6 +314,7 @@ void KernelBroker::serve(int fd, pid_t peer) {
   int64_t conn_bytes = 0;
   void* ws = nullptr;
   void* scalar = nullptr;
+  double* result = take_slot();  // pinned host slot (nullptr: fall back to a device scalar + copy)
   g_bk.malloc_(&ws, g_bk.reduce_ws());
   g_bk.malloc_(&scalar, 256);
   std::vector<char> payload;
@@ -311,6 +338,15 @@ void KernelBroker::serve(int fd, pid_t peer) {
     return hipMemsetAsync(b->ptr, 0, b->size, stream) == hipSuccess;
   };
   auto will_read = [&](Buf* b) -> bool { return scrub(b); };
+  // the scalar a reduction just wrote (pinned slot, or device scalar + copy)
+  auto fetch_result = [&](double* v) -> bool {
+    if (result == nullptr)
+      return hipMemcpyAsync(v, scalar, 8, hipMemcpyDeviceToHost, stream) == hipSuccess &&
+             hipStreamSynchronize(stream) == hipSuccess;
+    if (hipStreamSynchronize(stream) != hipSuccess) return false;
+    *v = *(volatile double*)result;
+    return true;
+  };
   auto will_write = [&](Buf* b, uint64_t off, uint64_t n) -> bool {
     if (b->clean) return true;
     if (off == 0 && n >= b->size) {  // fully overwritten: nothing stale survives
@@ -485,11 +521,10 @@ void KernelBroker::serve(int fd, pid_t peer) {
           break;
         }
         if (!will_read(ba) || !will_read(bb)) { st = kLaunchFailed; break; }
-        int rc = g_bk.reduce((int)rop, (int)dt, ba->ptr, bb ? bb->ptr : nullptr, n, ws, scalar, stream);
+        int rc = g_bk.reduce((int)rop, (int)dt, ba->ptr, bb ? bb->ptr : nullptr, n, ws, result ? (void*)result : scalar,
+                             stream);
         double v = 0;
-        if (rc == 0 && (hipMemcpyAsync(&v, scalar, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-                        hipStreamSynchronize(stream) != hipSuccess))
-          rc = kLaunchFailed;
+        if (rc == 0 && !fetch_result(&v)) rc = kLaunchFailed;
         if (rc) st = rc;
         put(&v, 8);
         break;
@@ -500,11 +535,9 @@ void KernelBroker::serve(int fd, pid_t peer) {
         const uint64_t seed = r.get<uint64_t>(), off = r.get<uint64_t>();
         const double lo = r.get<double>(), hi = r.get<double>();
         if (!r.ok || n < 0) { st = kProtocol; break; }
-        int rc = g_bk.rand_reduce((int)rop, (int)dt, n, seed, off, lo, hi, ws, scalar, stream);
+        int rc = g_bk.rand_reduce((int)rop, (int)dt, n, seed, off, lo, hi, ws, result ? (void*)result : scalar, stream);
         double v = 0;
-        if (rc == 0 && (hipMemcpyAsync(&v, scalar, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-                        hipStreamSynchronize(stream) != hipSuccess))
-          rc = kLaunchFailed;
+        if (rc == 0 && !fetch_result(&v)) rc = kLaunchFailed;
         if (rc) st = rc;
         put(&v, 8);
         break;
@@ -612,6 +645,7 @@ void KernelBroker::serve(int fd, pid_t peer) {
   }
   g_bk.free_(ws);
   g_bk.free_(scalar);
+  give_slot(result);
   give_stream(stream);  // drained above
   close(fd);
   conns_--;
