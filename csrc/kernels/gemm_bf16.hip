@@ -244,6 +244,37 @@ __global__ __launch_bounds__(256) void transpose_bf16(const uint16_t* __restrict
   }
 }
 
+// Vectorised transpose for 8-aligned shapes: each lane moves an 8x8 block
+// with eight 16-B loads and eight 16-B stores and swaps the halfwords in
+// registers (v_perm), so there is no LDS round trip and no barrier.  Per load
+// instruction a wave touches 8 input rows x 128 B (8 lanes per row), per store
+// 8 output rows x 128 B: whole cache lines both ways, where the tiled kernel
+// above moves 2 B per lane (128 B per wave instruction).  Block = 4 waves side
+// by side along the columns: a 64 x 256 input tile.
+__global__ __launch_bounds__(256) void transpose_bf16_v8(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                         int rows, int cols, int ld_in, int ld_out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = blockIdx.y * 64 + (lane >> 3) * 8;
+  const int c = blockIdx.x * 256 + wave * 64 + (lane & 7) * 8;
+  if (r >= rows || c >= cols) return;  // rows, cols are multiples of 8: a block is all in or all out
+  uint4 v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const uint4*>(in + (int64_t)(r + i) * ld_in + c);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    // output row c + j = input column j: halfword j of each of the 8 rows
+    uint32_t w[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const uint32_t* a = reinterpret_cast<const uint32_t*>(&v[2 * m]);
+      const uint32_t* b = reinterpret_cast<const uint32_t*>(&v[2 * m + 1]);
+      // bytes of {b:a}: even j takes the low halfwords, odd j the high ones
+      w[m] = __builtin_amdgcn_perm(b[j >> 1], a[j >> 1], (j & 1) ? 0x07060302u : 0x05040100u);
+    }
+    *reinterpret_cast<uint4*>(out + (int64_t)(c + j) * ld_out + r) = uint4{w[0], w[1], w[2], w[3]};
+  }
+}
+
 bool gemm256_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16);  // gemm_bf16_256.hip
 void launch_gemm256(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
                     float beta, bool out_bf16, hipStream_t stream, int which);
@@ -314,7 +345,12 @@ BK_API int bk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N,
 BK_API int bk_transpose_bf16(const void* in, void* out, int rows, int cols, int ld_in, int ld_out,
                              hipStream_t stream) {
   if (!in || !out || rows <= 0 || cols <= 0 || ld_in < cols || ld_out < rows) return kBadArgument;
-  dim3 grid((cols + 63) / 64, (rows + 63) / 64);
-  transpose_bf16<<<grid, 256, 0, stream>>>((const uint16_t*)in, (uint16_t*)out, rows, cols, ld_in, ld_out);
+  if (rows % 8 == 0 && cols % 8 == 0 && ld_in % 8 == 0 && ld_out % 8 == 0 && aligned16(in) && aligned16(out)) {
+    dim3 grid((cols + 255) / 256, (rows + 63) / 64);
+    transpose_bf16_v8<<<grid, 256, 0, stream>>>((const uint16_t*)in, (uint16_t*)out, rows, cols, ld_in, ld_out);
+  } else {
+    dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+    transpose_bf16<<<grid, 256, 0, stream>>>((const uint16_t*)in, (uint16_t*)out, rows, cols, ld_in, ld_out);
+  }
   return launch_status();
 }

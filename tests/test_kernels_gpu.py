@@ -194,6 +194,39 @@ def test_gemm_transposed_view_operand(gpu):
     np.testing.assert_allclose(c, a_h.astype(np.float64) @ bt_h.T.astype(np.float64), rtol=1e-2, atol=5e-2)
 
 
+@pytest.mark.parametrize("rows,cols,ld_in,ld_out", [
+    (8, 8, 8, 8), (64, 256, 256, 64), (136, 200, 200, 136), (72, 520, 528, 80),  # 16-B vector path
+    (7, 13, 13, 7), (65, 130, 131, 65),                                            # tiled fallback
+])
+def test_transpose_bf16_bitwise(gpu, rows, cols, ld_in, ld_out):
+    """Both transpose kernels (8x8 register blocks for 8-aligned shapes, LDS
+    tiles otherwise) against numpy, bit for bit, with padded leading
+    dimensions whose padding must stay untouched."""
+    from bee_code_interpreter_fs_amd.ops.array import driver
+
+    rng = np.random.default_rng(rows * 1000 + cols)
+    src_h = rng.integers(0, 1 << 16, size=(rows, ld_in), dtype=np.uint16)
+    sentinel = np.full((cols, ld_out), 0xBEEF, dtype=np.uint16)
+    src, dst = gpu.empty((rows * ld_in,), "bfloat16"), gpu.empty((cols * ld_out,), "bfloat16")
+    driver().h2d(src.ptr, src_h)
+    driver().h2d(dst.ptr, sentinel)
+    driver().transpose(src.ptr, dst.ptr, rows, cols, ld_in, ld_out)
+    out = np.empty((cols, ld_out), dtype=np.uint16)
+    driver().d2h(dst.ptr, out)
+    np.testing.assert_array_equal(out[:, :rows], src_h[:, :cols].T)
+    np.testing.assert_array_equal(out[:, rows:], sentinel[:, rows:])
+
+
+def test_matmul_row_major_b_large(gpu):
+    """bk.matmul(a, b) with a plain row-major b (transpose + TN GEMM) on a
+    shape that takes the vectorised transpose and the 256^2 GEMM."""
+    rng = np.random.default_rng(5)
+    a_h = _bf16_round(rng.uniform(-1, 1, (2048, 1024)).astype(np.float32))
+    b_h = _bf16_round(rng.uniform(-1, 1, (1024, 4096)).astype(np.float32))
+    c = gpu.matmul(gpu.asarray(a_h, "bfloat16"), gpu.asarray(b_h, "bfloat16"), out_dtype="float32").numpy()
+    np.testing.assert_allclose(c, a_h.astype(np.float64) @ b_h.astype(np.float64), rtol=1e-2, atol=2e-3 * 32)
+
+
 def test_quota_enforced(gpu):
     from bee_code_interpreter_fs_amd.ops import QuotaExceeded
 

@@ -99,6 +99,17 @@ def main():
             a.ptr, b.ptr, c_probe.ptr, size, size, size, size, size, size, 2), a_mod=a.ptr % 256, c_mod=c_probe.ptr % 256)
         ms, mn = timed(lambda: bk.gemm_bf16_tn(a, b, "bfloat16"), reps=20)
         emit(kernel=f"gemm_bf16_tn {size}^3", ms=ms, min_ms=mn, TFLOPs=flops / ms / 1e9, TFLOPs_best=flops / mn / 1e9)
+        bt_buf = bk.empty((size * size + 8,), "bfloat16")
+        from bee_code_interpreter_fs_amd.ops.array import driver
+
+        drv = driver()
+        ms_tr, mn_tr = timed(lambda: drv.transpose(b.ptr, bt_buf.ptr, size, size, size, size), reps=20)
+        emit(kernel=f"transpose_bf16 {size}^2", ms=ms_tr, min_ms=mn_tr, GBps=4 * size * size / ms_tr / 1e6)
+        # same copy through the LDS-tiled fallback (taken for a destination
+        # that is not 16-B aligned)
+        ms_tr, mn_tr = timed(lambda: drv.transpose(b.ptr, bt_buf.ptr + 2, size, size, size, size), reps=20)
+        emit(kernel=f"transpose_bf16 tiled fallback {size}^2", ms=ms_tr, min_ms=mn_tr, GBps=4 * size * size / ms_tr / 1e6)
+        del bt_buf
         ms2, _ = timed(lambda: bk.matmul(a, b), reps=10)
         emit(kernel=f"bk.matmul (transpose+gemm) {size}^3", ms=ms2, TFLOPs=flops / ms2 / 1e9)
         ta = torch.empty(size, size, dtype=torch.bfloat16, device="cuda").uniform_(-1, 1)
