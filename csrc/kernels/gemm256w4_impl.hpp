@@ -76,6 +76,10 @@ enum : int {
   kAsmMfma = 16,
   kEarlyGlds = 32,   // kAsmMfma|kInterleave: all K-tile loads in the first 8 of the second k-half's 16 groups
   kReadsEarly = 64,  // kAsmMfma|kInterleave: k-half-1 fragment reads done by group 11 of 16
+  // tile order (lab): M-group size other than kGroupM
+  kGroup2 = 128,
+  kGroup8 = 256,
+  kGroup16 = 512,
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
@@ -323,9 +327,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
 
   const int nbm = M / TM, nbn = N / TN, nblocks = nbm * nbn;
   const int b = xcd_remap(blockIdx.x, nblocks);
-  const int group = kGroupM * nbn;
-  const int first_m = (b / group) * kGroupM;
-  const int gm = min(nbm - first_m, kGroupM);
+  constexpr int kGm = (O & kGroup2) ? 2 : (O & kGroup8) ? 8 : (O & kGroup16) ? 16 : kGroupM;
+  const int group = kGm * nbn;
+  const int first_m = (b / group) * kGm;
+  const int gm = min(nbm - first_m, kGm);
   const int tm = first_m + (b % group) % gm, tn = (b % group) / gm;
   const int m0 = tm * TM, n0 = tn * TN;
 

@@ -27,7 +27,10 @@ constexpr int kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave, g4::kNoCarry, g4::
                            g4::kAsmMfma | g4::kInterleave, g4::kAsmMfma | g4::kNoCarry,
                            g4::kAsmMfma | g4::kInterleave | g4::kEarlyGlds,
                            g4::kAsmMfma | g4::kInterleave | g4::kReadsEarly,
-                           g4::kAsmMfma | g4::kInterleave | g4::kReadsEarly | g4::kEarlyGlds};
+                           g4::kAsmMfma | g4::kInterleave | g4::kReadsEarly | g4::kEarlyGlds,
+                           g4::kAsmMfma | g4::kInterleave | g4::kGroup2,
+                           g4::kAsmMfma | g4::kInterleave | g4::kGroup8,
+                           g4::kAsmMfma | g4::kInterleave | g4::kGroup16};
 template <int I>
 void run_w4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool bf,
             hipStream_t s) {
@@ -57,6 +60,9 @@ BK_API int gemmlab_run(int variant, const void* A, const void* Bt, void* C, int 
     case 13: run_w4<7>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 14: run_w4<8>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 15: run_w4<9>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 16: run_w4<10>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 17: run_w4<11>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 18: run_w4<12>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     default: return kBadArgument;
   }
   return launch_status();
