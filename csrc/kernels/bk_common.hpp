@@ -142,4 +142,14 @@ __device__ __forceinline__ uint16_t float_to_bf16_bits(float f) {
   return *reinterpret_cast<uint16_t*>(&h);
 }
 
+// f64 -> bf16 through f32 (two RNE roundings, as the host's
+// astype(float32) -> bf16): the empty asm pins the f32 intermediate, which
+// the compiler otherwise may fold into one f64 -> bf16 rounding (it did in
+// one of two kernels: 2 of 27200 values 1 ulp apart).
+__device__ __forceinline__ uint16_t double_to_bf16_bits(double d) {
+  float f = (float)d;
+  asm volatile("" : "+v"(f));
+  return float_to_bf16_bits(f);
+}
+
 }  // namespace bk

@@ -159,7 +159,10 @@ template <typename TI, typename TO>
 __global__ __launch_bounds__(256) void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    y[i] = Elem<TO>::store((typename Elem<TO>::C)Elem<TI>::load(x[i]));
+    if constexpr (std::is_same<TI, double>::value && std::is_same<TO, uint16_t>::value)
+      y[i] = double_to_bf16_bits(x[i]);
+    else
+      y[i] = Elem<TO>::store((typename Elem<TO>::C)Elem<TI>::load(x[i]));
   }
 }
 

@@ -275,6 +275,43 @@ __global__ __launch_bounds__(256) void transpose_bf16_v8(const uint16_t* __restr
   }
 }
 
+// The same 8x8 register-block transpose fused with the f32/f64 -> bf16
+// conversion the TN GEMM needs for a non-bf16 row-major B: one pass reads
+// the wide input and writes Bt in bf16 (cast-then-transpose read it, wrote a
+// bf16 copy, read that and wrote Bt).  Rounding is the cast kernel's
+// ((float) then RNE to bf16), so the result is bitwise that of the two passes.
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_to_bf16_v8(const T* __restrict__ in, uint16_t* __restrict__ out,
+                                                            int rows, int cols, int ld_in, int ld_out) {
+  constexpr int kVec = 16 / sizeof(T);  // elements per 16-B load
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = blockIdx.y * 64 + (lane >> 3) * 8;
+  const int c = blockIdx.x * 256 + wave * 64 + (lane & 7) * 8;
+  if (r >= rows || c >= cols) return;
+  uint16_t h[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    T x[8];
+#pragma unroll
+    for (int q = 0; q < 8 / kVec; ++q)
+      *reinterpret_cast<uint4*>(&x[q * kVec]) = *reinterpret_cast<const uint4*>(in + (int64_t)(r + i) * ld_in + c + q * kVec);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (sizeof(T) == 8)
+        h[i][j] = double_to_bf16_bits(x[j]);
+      else
+        h[i][j] = float_to_bf16_bits(x[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t w[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) w[m] = (uint32_t)h[2 * m][j] | ((uint32_t)h[2 * m + 1][j] << 16);
+    *reinterpret_cast<uint4*>(out + (int64_t)(c + j) * ld_out + r) = uint4{w[0], w[1], w[2], w[3]};
+  }
+}
+
 bool gemm256_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16);  // gemm_bf16_256.hip
 void launch_gemm256(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
                     float beta, bool out_bf16, hipStream_t stream, int which);
@@ -352,5 +389,22 @@ BK_API int bk_transpose_bf16(const void* in, void* out, int rows, int cols, int 
     dim3 grid((cols + 63) / 64, (rows + 63) / 64);
     transpose_bf16<<<grid, 256, 0, stream>>>((const uint16_t*)in, (uint16_t*)out, rows, cols, ld_in, ld_out);
   }
+  return launch_status();
+}
+
+// out[cols x rows] (bf16) = transpose of in[rows x cols] (src_dtype kBF16,
+// kF32 or kF64).  Wide inputs need the 8-aligned, 16-B aligned shape of the
+// vector kernel (kBadArgument otherwise: the caller casts, then transposes).
+BK_API int bk_transpose_to_bf16(int src_dtype, const void* in, void* out, int rows, int cols, int ld_in, int ld_out,
+                                hipStream_t stream) {
+  if (src_dtype == kBF16) return bk_transpose_bf16(in, out, rows, cols, ld_in, ld_out, stream);
+  if (!in || !out || rows <= 0 || cols <= 0 || ld_in < cols || ld_out < rows) return kBadArgument;
+  if (src_dtype != kF32 && src_dtype != kF64) return kBadArgument;
+  if (rows % 8 || cols % 8 || ld_in % 8 || ld_out % 8 || !aligned16(in) || !aligned16(out)) return kBadArgument;
+  dim3 grid((cols + 255) / 256, (rows + 63) / 64);
+  if (src_dtype == kF32)
+    transpose_to_bf16_v8<float><<<grid, 256, 0, stream>>>((const float*)in, (uint16_t*)out, rows, cols, ld_in, ld_out);
+  else
+    transpose_to_bf16_v8<double><<<grid, 256, 0, stream>>>((const double*)in, (uint16_t*)out, rows, cols, ld_in, ld_out);
   return launch_status();
 }

@@ -217,6 +217,67 @@ def test_transpose_bf16_bitwise(gpu, rows, cols, ld_in, ld_out):
     np.testing.assert_array_equal(out[:, rows:], sentinel[:, rows:])
 
 
+@pytest.mark.parametrize("src_dtype", ["float32", "float64"])
+@pytest.mark.parametrize("rows,cols,ld_in,ld_out", [(8, 8, 8, 8), (136, 200, 200, 136), (72, 520, 528, 80)])
+def test_transpose_to_bf16_bitwise(gpu, src_dtype, rows, cols, ld_in, ld_out):
+    """Fused f32/f64 -> bf16 transpose == cast kernel then transpose, bit for
+    bit (same rounding: (float) then RNE), padding untouched."""
+    from bee_code_interpreter_fs_amd.ops._native import DTYPE_CODES
+    from bee_code_interpreter_fs_amd.ops.array import driver
+
+    rng = np.random.default_rng(rows + cols)
+    src_h = rng.standard_normal((rows, ld_in)).astype(src_dtype)
+    src_h[0, 0], src_h[-1, cols - 1] = 3e38, -0.0  # near the top of the bf16 range; signed zero
+    src = gpu.empty((rows * ld_in,), src_dtype)
+    driver().h2d(src.ptr, src_h)
+    dst = gpu.empty((cols * ld_out,), "bfloat16")
+    driver().h2d(dst.ptr, np.full((cols, ld_out), 0xBEEF, dtype=np.uint16))
+    driver().transpose(src.ptr, dst.ptr, rows, cols, ld_in, ld_out, DTYPE_CODES[src_dtype])
+    fused = np.empty((cols, ld_out), dtype=np.uint16)
+    driver().d2h(dst.ptr, fused)
+    # two-pass reference on the device: the cast kernel, then the bf16 transpose
+    cast = gpu.empty((rows * ld_in,), "bfloat16")
+    driver().cast(DTYPE_CODES[src_dtype], DTYPE_CODES["bfloat16"], src.ptr, cast.ptr, rows * ld_in)
+    two = gpu.empty((cols * ld_out,), "bfloat16")
+    driver().transpose(cast.ptr, two.ptr, rows, cols, ld_in, ld_out)
+    ref = np.empty((cols, ld_out), dtype=np.uint16)
+    driver().d2h(two.ptr, ref)
+    np.testing.assert_array_equal(fused[:, :rows], ref[:, :rows])
+    np.testing.assert_array_equal(fused[:, rows:], 0xBEEF)
+    # and against the host rounding of the f32 value
+    host = _f32_to_bf16_host(src_h[:, :cols].astype(np.float32)).T
+    np.testing.assert_array_equal(fused[:, :rows], host)
+
+
+def _f32_to_bf16_host(a):
+    from bee_code_interpreter_fs_amd.ops.array import _f32_to_bf16_bits
+
+    return _f32_to_bf16_bits(a)
+
+
+def test_transpose_to_bf16_rejects_unaligned_wide_input(gpu):
+    from bee_code_interpreter_fs_amd.ops import _native
+
+    x = gpu.empty((12 * 12,), "float32")
+    y = gpu.empty((12 * 12,), "bfloat16")
+    assert _native.lib().bk_transpose_to_bf16(0, x.ptr, y.ptr, 12, 12, 12, 12, None) != 0
+
+
+@pytest.mark.parametrize("b_kind", ["float64", "float32", "float32_T"])
+def test_matmul_wide_b_operand(gpu, b_kind):
+    """matmul with an f64/f32 row-major b (fused convert+transpose) and with
+    an f32 b.T view (conversion only) against fp64."""
+    rng = np.random.default_rng(9)
+    a_h = _bf16_round(rng.uniform(-1, 1, (512, 256)).astype(np.float32))
+    b_h = _bf16_round(rng.uniform(-1, 1, (256, 768)).astype(np.float32))
+    if b_kind == "float32_T":
+        b = gpu.asarray(np.ascontiguousarray(b_h.T), "float32").T
+    else:
+        b = gpu.asarray(b_h, b_kind)
+    c = gpu.matmul(gpu.asarray(a_h, "bfloat16"), b, out_dtype="float32").numpy()
+    np.testing.assert_allclose(c, a_h.astype(np.float64) @ b_h.astype(np.float64), rtol=1e-2, atol=2e-3 * 16)
+
+
 def test_matmul_row_major_b_large(gpu):
     """bk.matmul(a, b) with a plain row-major b (transpose + TN GEMM) on a
     shape that takes the vectorised transpose and the 256^2 GEMM."""

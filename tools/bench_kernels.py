@@ -112,6 +112,15 @@ def main():
         del bt_buf
         ms2, _ = timed(lambda: bk.matmul(a, b), reps=10)
         emit(kernel=f"bk.matmul (transpose+gemm) {size}^3", ms=ms2, TFLOPs=flops / ms2 / 1e9)
+        b32 = b.astype("float32")
+        ms3, _ = timed(lambda: bk.matmul(a, b32), reps=10)
+        emit(kernel=f"bk.matmul f32 b (fused convert+transpose, gemm) {size}^3", ms=ms3, TFLOPs=flops / ms3 / 1e9)
+        from bee_code_interpreter_fs_amd.ops._native import DTYPE_CODES
+
+        bt16 = bk.empty((size, size), "bfloat16")
+        ms4, _ = timed(lambda: drv.transpose(b32.ptr, bt16.ptr, size, size, size, size, DTYPE_CODES["float32"]), reps=20)
+        emit(kernel=f"transpose_to_bf16 from f32 {size}^2", ms=ms4, GBps=6 * size * size / ms4 / 1e6)
+        del b32, bt16
         ta = torch.empty(size, size, dtype=torch.bfloat16, device="cuda").uniform_(-1, 1)
         tb = torch.empty(size, size, dtype=torch.bfloat16, device="cuda").uniform_(-1, 1)
         ms_t, mn_t = torch_timed(lambda: ta @ tb.T, reps=20)
