@@ -195,11 +195,8 @@ class DeviceArray:
         if self._transposed:
             rows, cols = self.shape[1], self.shape[0]  # underlying buffer is (rows, cols)
             src = self._buf
-            if self.dtype == "bfloat16":
-                out = _Buffer(self.nbytes)
-                driver().transpose(src.ptr, out.ptr, rows, cols, cols, rows)
-            else:
-                out = _upload(np.ascontiguousarray(_download(src, (rows, cols), self.dtype).T), self.dtype)
+            out = _Buffer(self.nbytes)  # on-device transpose, 2/4/8-byte elements
+            driver().transpose(src.ptr, out.ptr, rows, cols, cols, rows, self.code, self.code)
             self._buf = out
             self._transposed = False
         return self

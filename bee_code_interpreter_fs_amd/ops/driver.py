@@ -99,8 +99,9 @@ class NativeDriver:
             "bk_gemm_bf16_tn",
         )
 
-    def transpose(self, src: int, dst: int, rows: int, cols: int, ldi: int, ldo: int, src_dtype: int = 2) -> None:
-        check(self.lib.bk_transpose_to_bf16(src_dtype, _vp(src), _vp(dst), rows, cols, ldi, ldo, self.stream),
+    def transpose(self, src: int, dst: int, rows: int, cols: int, ldi: int, ldo: int, src_dtype: int = 2,
+                  dst_dtype: int = 2) -> None:
+        check(self.lib.bk_transpose(src_dtype, dst_dtype, _vp(src), _vp(dst), rows, cols, ldi, ldo, self.stream),
               "transpose")
 
     def copy(self, dst: int, src: int, nbytes: int) -> None:
@@ -285,8 +286,8 @@ class BrokerDriver:
     def gemm(self, A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt) -> None:
         self._post(GEMM, struct.pack("<QQQiiiiiiffii", A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, 0))
 
-    def transpose(self, src, dst, rows, cols, ldi, ldo, src_dtype=2) -> None:
-        self._post(TRANSPOSE, struct.pack("<QQiiiii", src, dst, rows, cols, ldi, ldo, src_dtype))
+    def transpose(self, src, dst, rows, cols, ldi, ldo, src_dtype=2, dst_dtype=2) -> None:
+        self._post(TRANSPOSE, struct.pack("<QQiiiiii", src, dst, rows, cols, ldi, ldo, src_dtype, dst_dtype))
 
     def copy(self, dst, src, nbytes) -> None:
         self._post(COPY, struct.pack("<QQQQQ", dst, 0, src, 0, nbytes))

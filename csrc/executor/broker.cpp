@@ -118,7 +118,7 @@ struct Bk {
   int (*rand_reduce)(int, int, int64_t, uint64_t, uint64_t, double, double, void*, void*, hipStream_t);
   int (*reduce)(int, int, const void*, const void*, int64_t, void*, void*, hipStream_t);
   int (*gemm)(const void*, const void*, void*, int, int, int, int, int, int, float, float, int, hipStream_t);
-  int (*transpose)(int, const void*, void*, int, int, int, int, hipStream_t);
+  int (*transpose)(int, int, const void*, void*, int, int, int, int, hipStream_t);
 } g_bk;
 
 template <typename F>
@@ -159,7 +159,7 @@ bool KernelBroker::start(std::string* err) {
             sym(lib_, "bk_rand_normal", &g_bk.rand_normal) && sym(lib_, "bk_unary", &g_bk.unary) &&
             sym(lib_, "bk_binary", &g_bk.binary) && sym(lib_, "bk_cast", &g_bk.cast) && sym(lib_, "bk_fill", &g_bk.fill) &&
             sym(lib_, "bk_reduce_workspace_bytes", &g_bk.reduce_ws) && sym(lib_, "bk_reduce", &g_bk.reduce) &&
-            sym(lib_, "bk_gemm_bf16_tn", &g_bk.gemm) && sym(lib_, "bk_transpose_to_bf16", &g_bk.transpose) &&
+            sym(lib_, "bk_gemm_bf16_tn", &g_bk.gemm) && sym(lib_, "bk_transpose", &g_bk.transpose) &&
             sym(lib_, "bk_rand_reduce", &g_bk.rand_reduce);
   if (!ok) {
     *err = "libbeekern.so is missing broker entry points";
@@ -567,19 +567,21 @@ void KernelBroker::serve(int fd, pid_t peer) {
       case kTranspose: {
         const uint64_t in = r.get<uint64_t>(), o = r.get<uint64_t>();
         const int32_t rows = r.get<int32_t>(), cols = r.get<int32_t>(), ldi = r.get<int32_t>(), ldo = r.get<int32_t>();
-        const int32_t sdt = r.get<int32_t>();  // input dtype (f32 / f64 / bf16); the output is bf16
+        // dtypes: out == in (bit move) or out bf16 from f32 / f64 / bf16
+        const int32_t sdt = r.get<int32_t>(), ddt = r.get<int32_t>();
         Buf *bi, *bo;
-        if (!r.ok || rows <= 0 || cols <= 0 || ldi < cols || ldo < rows || (sdt != 0 && sdt != 1 && sdt != 2) ||
+        if (!r.ok || rows <= 0 || cols <= 0 || ldi < cols || ldo < rows || !dsize(sdt) ||
+            !(ddt == sdt || (ddt == 2 && sdt <= 2)) ||
             !lookup(in, ((uint64_t)(rows - 1) * ldi + cols) * dsize(sdt), &bi) ||
-            !lookup(o, ((uint64_t)(cols - 1) * ldo + rows) * 2, &bo)) {
+            !lookup(o, ((uint64_t)(cols - 1) * ldo + rows) * dsize(ddt), &bo)) {
           st = kBadHandle;
           break;
         }
-        if (!will_read(bi) || !will_write(bo, 0, ldo == rows ? (uint64_t)rows * cols * 2 : 0)) {
+        if (!will_read(bi) || !will_write(bo, 0, ldo == rows ? (uint64_t)rows * cols * dsize(ddt) : 0)) {
           st = kLaunchFailed;
           break;
         }
-        launched(g_bk.transpose(sdt, bi->ptr, bo->ptr, rows, cols, ldi, ldo, stream));
+        launched(g_bk.transpose(sdt, ddt, bi->ptr, bo->ptr, rows, cols, ldi, ldo, stream));
         break;
       }
       case kCopy: {

@@ -312,6 +312,45 @@ __global__ __launch_bounds__(256) void transpose_to_bf16_v8(const T* __restrict_
   }
 }
 
+// Same-dtype transpose of 4- and 8-byte elements (f32/i32, f64/i64): the
+// 8x8 register-block scheme with 2 (4 B) or 4 (8 B) 16-B loads and stores per
+// block row, so DeviceArray.T of a wide array no longer goes through the host.
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_wide_v8(const T* __restrict__ in, T* __restrict__ out, int rows,
+                                                         int cols, int ld_in, int ld_out) {
+  constexpr int kVec = 16 / sizeof(T);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = blockIdx.y * 64 + (lane >> 3) * 8;
+  const int c = blockIdx.x * 256 + wave * 64 + (lane & 7) * 8;
+  if (r >= rows || c >= cols) return;
+  T v[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int q = 0; q < 8 / kVec; ++q)
+      *reinterpret_cast<uint4*>(&v[i][q * kVec]) = *reinterpret_cast<const uint4*>(in + (int64_t)(r + i) * ld_in + c + q * kVec);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    T w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = v[i][j];
+#pragma unroll
+    for (int q = 0; q < 8 / kVec; ++q)
+      *reinterpret_cast<uint4*>(out + (int64_t)(c + j) * ld_out + r + q * kVec) = *reinterpret_cast<const uint4*>(&w[q * kVec]);
+  }
+}
+
+// any shape / alignment: one element per thread, writes coalesced
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_wide_scalar(const T* __restrict__ in, T* __restrict__ out, int rows,
+                                                             int cols, int ld_in, int ld_out) {
+  const int64_t n = (int64_t)rows * cols, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int oc = (int)(i / rows), orow = (int)(i % rows);  // out[oc][orow] = in[orow][oc]
+    out[(int64_t)oc * ld_out + orow] = in[(int64_t)orow * ld_in + oc];
+  }
+}
+
 bool gemm256_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16);  // gemm_bf16_256.hip
 void launch_gemm256(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
                     float beta, bool out_bf16, hipStream_t stream, int which);
@@ -406,5 +445,32 @@ BK_API int bk_transpose_to_bf16(int src_dtype, const void* in, void* out, int ro
     transpose_to_bf16_v8<float><<<grid, 256, 0, stream>>>((const float*)in, (uint16_t*)out, rows, cols, ld_in, ld_out);
   else
     transpose_to_bf16_v8<double><<<grid, 256, 0, stream>>>((const double*)in, (uint16_t*)out, rows, cols, ld_in, ld_out);
+  return launch_status();
+}
+
+// out[cols x rows] = transpose of in[rows x cols].  dst_dtype kBF16 converts
+// (bk_transpose_to_bf16); dst_dtype == src_dtype moves the bits (2-, 4- or
+// 8-byte elements).
+BK_API int bk_transpose(int src_dtype, int dst_dtype, const void* in, void* out, int rows, int cols, int ld_in,
+                        int ld_out, hipStream_t stream) {
+  if (dst_dtype == kBF16) return bk_transpose_to_bf16(src_dtype, in, out, rows, cols, ld_in, ld_out, stream);
+  if (dst_dtype != src_dtype) return kBadArgument;
+  const int es = dtype_size(src_dtype);
+  if (es == 2) return bk_transpose_bf16(in, out, rows, cols, ld_in, ld_out, stream);
+  if (es != 4 && es != 8) return kBadArgument;
+  if (!in || !out || rows <= 0 || cols <= 0 || ld_in < cols || ld_out < rows) return kBadArgument;
+  if (rows % 8 == 0 && cols % 8 == 0 && ld_in % 8 == 0 && ld_out % 8 == 0 && aligned16(in) && aligned16(out)) {
+    dim3 grid((cols + 255) / 256, (rows + 63) / 64);
+    if (es == 4)
+      transpose_wide_v8<uint32_t><<<grid, 256, 0, stream>>>((const uint32_t*)in, (uint32_t*)out, rows, cols, ld_in, ld_out);
+    else
+      transpose_wide_v8<uint64_t><<<grid, 256, 0, stream>>>((const uint64_t*)in, (uint64_t*)out, rows, cols, ld_in, ld_out);
+  } else {
+    const unsigned g = stream_grid((int64_t)rows * cols, 256);
+    if (es == 4)
+      transpose_wide_scalar<uint32_t><<<g, 256, 0, stream>>>((const uint32_t*)in, (uint32_t*)out, rows, cols, ld_in, ld_out);
+    else
+      transpose_wide_scalar<uint64_t><<<g, 256, 0, stream>>>((const uint64_t*)in, (uint64_t*)out, rows, cols, ld_in, ld_out);
+  }
   return launch_status();
 }

@@ -255,6 +255,20 @@ def _f32_to_bf16_host(a):
     return _f32_to_bf16_bits(a)
 
 
+@pytest.mark.parametrize("dtype", ["float32", "float64", "bfloat16"])
+@pytest.mark.parametrize("shape", [(8, 8), (64, 256), (136, 200), (7, 13), (65, 130)])
+def test_transposed_view_materialises_on_device_bitwise(gpu, dtype, shape):
+    """DeviceArray.T of f32/f64 arrays: the 4-/8-byte register-block kernel
+    (8-aligned shapes) or the scalar fallback, bit for bit."""
+    rng = np.random.default_rng(shape[0] * 31 + shape[1])
+    h = rng.standard_normal(shape).astype(np.float32 if dtype != "float64" else np.float64)
+    x = gpu.asarray(h, dtype)
+    ref = x.numpy().T
+    got = x.T.numpy()
+    assert got.shape == ref.shape
+    np.testing.assert_array_equal(got, ref)
+
+
 def test_transpose_to_bf16_rejects_unaligned_wide_input(gpu):
     from bee_code_interpreter_fs_amd.ops import _native
 

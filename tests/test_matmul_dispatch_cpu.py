@@ -33,7 +33,7 @@ class FakeDriver:
     def cast(self, s, d, x, y, n):
         self.calls.append(("cast", s, d, n))
 
-    def transpose(self, src, dst, rows, cols, ldi, ldo, src_dtype=2):
+    def transpose(self, src, dst, rows, cols, ldi, ldo, src_dtype=2, dst_dtype=2):
         self.calls.append(("transpose", rows, cols, src_dtype))
 
     def gemm(self, a, bt, c, M, N, K, lda, ldb, ldc, alpha, beta, odt):
@@ -96,3 +96,11 @@ def test_shape_mismatch_raises(fake):
 def test_host_operand_is_uploaded(fake):
     arr.matmul(np.zeros((16, 8), np.float32), arr.DeviceArray((8, 24), "bfloat16"))
     assert _ops(fake) == ["cast", "transpose", "gemm"]
+
+
+@pytest.mark.parametrize("dtype", ["float32", "float64"])
+def test_wide_transposed_view_materialises_on_device(fake, dtype):
+    x = arr.DeviceArray((24, 40), dtype)
+    x.T._materialize()
+    code = DTYPE_CODES[dtype]
+    assert fake.calls == [("transpose", 24, 40, code)]
