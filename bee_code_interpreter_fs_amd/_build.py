@@ -161,6 +161,21 @@ def _targets() -> List[Target]:
                 link_flags=["-shared", "-fPIC"],
             )
         )
+    jl = os.path.join(CSRC, "jail")
+    if os.path.isdir(jl):
+        import sysconfig
+
+        targets.append(
+            Target(
+                name="jail",
+                output=os.path.join(PKG, "runtime", "_jail" + sysconfig.get_config_var("EXT_SUFFIX")),
+                sources=[os.path.join(jl, "jail.cpp")],
+                compiler=CXX,
+                compile_flags=["-O2", "-fPIC", "-std=c++17", "-Wall", "-Wextra", "-Wno-missing-field-initializers",
+                               f"-I{sysconfig.get_paths()['include']}"],
+                link_flags=["-shared", "-fPIC"],
+            )
+        )
     if os.path.isdir(rb) and os.listdir(rb):
         targets.append(
             Target(

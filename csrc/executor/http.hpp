@@ -67,10 +67,14 @@ class HttpServer {
   void serve_forever();                                    // blocks
   void stop();
   std::string bound_address() const { return bound_; }
+  // Unix-socket listeners: refuse peers for which this returns false
+  // (called with the peer's pid/uid from SO_PEERCRED before any byte is read)
+  void set_peer_filter(std::function<bool(pid_t, uid_t)> f) { peer_filter_ = std::move(f); }
 
  private:
   void handle_conn(int fd);
   HttpHandler handler_;
+  std::function<bool(pid_t, uid_t)> peer_filter_;
   int listen_fd_ = -1;
   std::string bound_;
   std::string unix_path_;

@@ -1,0 +1,418 @@
+// Sandbox jail: the isolation boundary applied to every single-use sandbox
+// process right after it is forked from its zygote, before any user code
+// runs.  Python extension `_jail` (bee_code_interpreter_fs_amd/runtime).
+//
+// The reference isolates each execution in a fresh Kubernetes pod running as
+// a non-root UID (`src/code_interpreter/services/kubernetes_code_executor.py:
+// 220-253`, `executor/Dockerfile:91-98`): the pod cannot see the service's
+// file-object store, other pods, or the service's processes.  Forked
+// sandboxes share one host, so the same guarantees are rebuilt from kernel
+// primitives, each applied when the kernel/privileges allow it:
+//
+//   * a per-sandbox UID/GID (service running with CAP_SETUID): DAC keeps the
+//     sandbox out of the store (0700), other sandboxes' dirs (0700, other
+//     UIDs), the control sockets (0600) and other processes (signals,
+//     /proc/<pid>/environ);  RLIMIT_NPROC becomes a per-sandbox pids cap;
+//   * Landlock (unprivileged, ABI >= 1): default-deny filesystem view --
+//     read/execute on the system and Python trees, read-write only on the
+//     sandbox's own workspace/runtime-packages/tmp and /dev/shm; protected
+//     trees (store, sandbox root, control dir) are carved out of every
+//     allowed hierarchy.  Landlock also scopes ptrace (so /proc/<pid>/environ,
+//     /mem, /fd of processes outside the sandbox are denied), and from ABI 6
+//     signals and abstract Unix sockets to the sandbox's own domain;
+//   * seccomp-bpf: kernel-attack-surface syscalls (ptrace, process_vm_*,
+//     mount/namespace/bpf/perf/keyring/module/kexec/io_uring ...) fail with
+//     EPERM; non-native syscall ABIs (x32, i386) kill the process;
+//   * rlimits: no core dumps, a per-process data-segment cap (RLIMIT_DATA:
+//     private writable memory -- a 100 GB bytearray is a MemoryError), file
+//     size cap, and the pids cap above.
+//
+// prepare() runs once in the zygote: it resolves the static rule set and
+// opens one O_PATH descriptor per rule, so a sandbox pays only one
+// landlock_add_rule per rule (no path walks) when it applies the jail.
+#include <Python.h>
+
+#include <errno.h>
+#include <fcntl.h>
+#include <grp.h>
+#include <linux/audit.h>
+#include <linux/capability.h>
+#include <linux/filter.h>
+#include <linux/landlock.h>
+#include <linux/seccomp.h>
+#include <stddef.h>
+#include <sys/prctl.h>
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <string>
+#include <vector>
+
+namespace {
+
+// ---- Landlock --------------------------------------------------------------------
+
+// access rights, by ABI version that introduced them
+constexpr uint64_t kFsV1 = (1ULL << 13) - 1;          // EXECUTE .. MAKE_SYM
+constexpr uint64_t kFsRefer = 1ULL << 13;             // ABI 2
+constexpr uint64_t kFsTruncate = 1ULL << 14;          // ABI 3
+constexpr uint64_t kScopeAbstractUnix = 1ULL << 0;    // ABI 6
+constexpr uint64_t kScopeSignal = 1ULL << 1;          // ABI 6
+
+constexpr uint64_t kRead = LANDLOCK_ACCESS_FS_EXECUTE | LANDLOCK_ACCESS_FS_READ_FILE | LANDLOCK_ACCESS_FS_READ_DIR;
+
+// ruleset_attr grew over ABI versions; pass the size the kernel knows
+struct RulesetAttr {
+  uint64_t handled_access_fs;
+  uint64_t handled_access_net;
+  uint64_t scoped;
+};
+
+int ll_abi() {
+  static int abi = -2;
+  if (abi == -2) {
+    const long r = syscall(__NR_landlock_create_ruleset, nullptr, 0, LANDLOCK_CREATE_RULESET_VERSION);
+    abi = r < 0 ? 0 : (int)r;
+  }
+  return abi;
+}
+
+uint64_t handled_fs(int abi) {
+  uint64_t m = kFsV1;
+  if (abi >= 2) m |= kFsRefer;
+  if (abi >= 3) m |= kFsTruncate;
+  // IOCTL_DEV (ABI 5) is deliberately not handled: HIP drives /dev/kfd and
+  // the render node with ioctls, and device access is already mediated by
+  // the device nodes' own permissions
+  return m;
+}
+
+struct Rule {
+  int fd;
+  uint64_t access;  // requested; masked by handled_fs() at apply time
+  std::string path;
+};
+
+std::vector<Rule> g_rules;  // static rules prepared in the zygote
+constexpr int kRuleFdBase = 700;
+
+// ---- seccomp ---------------------------------------------------------------------
+
+// syscalls a sandbox never needs; they fail with EPERM
+const int kDenied[] = {
+    SYS_ptrace, SYS_process_vm_readv, SYS_process_vm_writev, SYS_kcmp, SYS_pidfd_getfd, SYS_process_madvise,
+    SYS_mount, SYS_umount2, SYS_pivot_root, SYS_chroot, SYS_unshare, SYS_setns, SYS_fsopen, SYS_fsconfig,
+    SYS_fsmount, SYS_fspick, SYS_move_mount, SYS_open_tree, SYS_mount_setattr, SYS_bpf, SYS_perf_event_open,
+    SYS_userfaultfd, SYS_keyctl, SYS_add_key, SYS_request_key, SYS_init_module, SYS_finit_module,
+    SYS_delete_module, SYS_kexec_load, SYS_kexec_file_load, SYS_reboot, SYS_swapon, SYS_swapoff, SYS_acct,
+    SYS_quotactl, SYS_syslog, SYS_settimeofday, SYS_clock_settime, SYS_clock_adjtime, SYS_adjtimex,
+    SYS_sethostname, SYS_setdomainname, SYS_iopl, SYS_ioperm, SYS_open_by_handle_at, SYS_name_to_handle_at,
+    SYS_fanotify_init, SYS_lookup_dcookie, SYS_vhangup, SYS_io_uring_setup, SYS_io_uring_enter,
+    SYS_io_uring_register, SYS_uselib, SYS_personality,
+};
+
+std::vector<sock_filter> seccomp_program() {
+  std::vector<sock_filter> p;
+  auto stmt = [&](uint16_t code, uint32_t k) { p.push_back(BPF_STMT(code, k)); };
+  auto jump = [&](uint16_t code, uint32_t k, uint8_t jt, uint8_t jf) { p.push_back(BPF_JUMP(code, k, jt, jf)); };
+  const size_t n = sizeof kDenied / sizeof kDenied[0];
+  // native ABI only
+  stmt(BPF_LD | BPF_W | BPF_ABS, offsetof(seccomp_data, arch));
+  jump(BPF_JMP | BPF_JEQ | BPF_K, AUDIT_ARCH_X86_64, 1, 0);
+  stmt(BPF_RET | BPF_K, SECCOMP_RET_KILL_PROCESS);
+  stmt(BPF_LD | BPF_W | BPF_ABS, offsetof(seccomp_data, nr));
+  // x32 syscalls (bit 30) alias the native ones: refuse them all
+  jump(BPF_JMP | BPF_JGE | BPF_K, 0x40000000u, (uint8_t)(n + 1), 0);
+  for (size_t i = 0; i < n; ++i) jump(BPF_JMP | BPF_JEQ | BPF_K, (uint32_t)kDenied[i], (uint8_t)(n - i), 0);
+  stmt(BPF_RET | BPF_K, SECCOMP_RET_ALLOW);
+  stmt(BPF_RET | BPF_K, SECCOMP_RET_ERRNO | (EPERM & SECCOMP_RET_DATA));
+  return p;
+}
+
+bool seccomp_available() {
+  // PR_GET_SECCOMP works everywhere seccomp is compiled in
+  return prctl(PR_GET_SECCOMP, 0, 0, 0, 0) >= 0;
+}
+
+// ---- helpers ---------------------------------------------------------------------
+
+bool list_of_str(PyObject* o, std::vector<std::string>* out) {
+  if (o == nullptr || o == Py_None) return true;
+  PyObject* seq = PySequence_Fast(o, "expected a sequence of str");
+  if (!seq) return false;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* it = PySequence_Fast_GET_ITEM(seq, i);
+    const char* s = PyUnicode_AsUTF8(it);
+    if (!s) {
+      Py_DECREF(seq);
+      return false;
+    }
+    out->push_back(s);
+  }
+  Py_DECREF(seq);
+  return true;
+}
+
+long long dict_int(PyObject* d, const char* key, long long dflt) {
+  PyObject* v = PyDict_GetItemString(d, key);  // borrowed
+  if (!v || v == Py_None) return dflt;
+  const long long r = PyLong_AsLongLong(v);
+  if (r == -1 && PyErr_Occurred()) {
+    PyErr_Clear();
+    return dflt;
+  }
+  return r;
+}
+
+bool dict_bool(PyObject* d, const char* key, bool dflt) {
+  PyObject* v = PyDict_GetItemString(d, key);
+  if (!v || v == Py_None) return dflt;
+  return PyObject_IsTrue(v) == 1;
+}
+
+PyObject* os_error(const char* what) {
+  const int e = errno;
+  PyErr_Format(PyExc_OSError, "jail: %s: %s", what, strerror(e));
+  return nullptr;
+}
+
+bool set_limit(int res, long long v) {
+  if (v <= 0) return true;
+  rlimit rl{(rlim_t)v, (rlim_t)v};
+  rlimit cur{};
+  if (getrlimit(res, &cur) == 0 && cur.rlim_max != RLIM_INFINITY && (rlim_t)v > cur.rlim_max) rl.rlim_max = rl.rlim_cur = cur.rlim_max;
+  return setrlimit(res, &rl) == 0;
+}
+
+// ---- Python API ------------------------------------------------------------------
+
+PyObject* py_probe(PyObject*, PyObject*) {
+  const int abi = ll_abi();
+  const bool root = geteuid() == 0;
+  return Py_BuildValue("{s:i,s:O,s:O,s:i,s:i}", "landlock_abi", abi, "seccomp", seccomp_available() ? Py_True : Py_False,
+                       "can_setuid", root ? Py_True : Py_False, "euid", (int)geteuid(), "prepared_rules",
+                       (int)g_rules.size());
+}
+
+// prepare([(path, access_mask), ...]) in the zygote: open the static rule set
+PyObject* py_prepare(PyObject*, PyObject* args) {
+  PyObject* rules;
+  if (!PyArg_ParseTuple(args, "O", &rules)) return nullptr;
+  for (auto& r : g_rules) close(r.fd);
+  g_rules.clear();
+  PyObject* seq = PySequence_Fast(rules, "expected a sequence of (path, access)");
+  if (!seq) return nullptr;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  int next_fd = kRuleFdBase;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    const char* path;
+    unsigned long long access;
+    if (!PyArg_ParseTuple(PySequence_Fast_GET_ITEM(seq, i), "sK", &path, &access)) {
+      Py_DECREF(seq);
+      return nullptr;
+    }
+    const int fd = open(path, O_PATH | O_CLOEXEC);
+    if (fd < 0) continue;  // vanished / unreadable: simply not allowed
+    // park the descriptors in one contiguous block so a sandbox closes them
+    // with a single close_range after applying the rules
+    const int hi = fcntl(fd, F_DUPFD_CLOEXEC, next_fd);
+    close(fd);
+    if (hi < 0) continue;
+    next_fd = hi + 1;
+    g_rules.push_back(Rule{hi, (uint64_t)access, path});
+  }
+  Py_DECREF(seq);
+  return PyLong_FromSsize_t((Py_ssize_t)g_rules.size());
+}
+
+// apply(opts) in a freshly forked sandbox.  opts keys:
+//   uid, gid (0/absent: keep), groups [gid...], own_rw [paths], extra_ro [paths],
+//   nproc, data_bytes, fsize_bytes, nofile, landlock (bool), seccomp (bool),
+//   scope_signal (bool), scope_abstract_unix (bool)
+// Returns a dict describing what was applied; raises OSError when a requested
+// privilege drop fails (fail closed).
+PyObject* py_apply(PyObject*, PyObject* args) {
+  PyObject* opts;
+  if (!PyArg_ParseTuple(args, "O!", &PyDict_Type, &opts)) return nullptr;
+  std::vector<std::string> own_rw, extra_ro, groups_s;
+  if (!list_of_str(PyDict_GetItemString(opts, "own_rw"), &own_rw)) return nullptr;
+  if (!list_of_str(PyDict_GetItemString(opts, "extra_ro"), &extra_ro)) return nullptr;
+  std::vector<gid_t> groups;
+  if (PyObject* g = PyDict_GetItemString(opts, "groups")) {
+    PyObject* seq = PySequence_Fast(g, "groups must be a sequence");
+    if (!seq) return nullptr;
+    for (Py_ssize_t i = 0; i < PySequence_Fast_GET_SIZE(seq); ++i)
+      groups.push_back((gid_t)PyLong_AsLong(PySequence_Fast_GET_ITEM(seq, i)));
+    Py_DECREF(seq);
+  }
+  const long long uid = dict_int(opts, "uid", 0), gid = dict_int(opts, "gid", uid);
+  const bool want_ll = dict_bool(opts, "landlock", true), want_sc = dict_bool(opts, "seccomp", true);
+  const bool scope_signal = dict_bool(opts, "scope_signal", true);
+  const bool scope_abstract = dict_bool(opts, "scope_abstract_unix", true);
+
+  // 1. resource limits (lowering limits needs no privilege)
+  {
+    rlimit z{0, 0};
+    setrlimit(RLIMIT_CORE, &z);
+  }
+  if (!set_limit(RLIMIT_DATA, dict_int(opts, "data_bytes", 0))) return os_error("RLIMIT_DATA");
+  if (!set_limit(RLIMIT_FSIZE, dict_int(opts, "fsize_bytes", 0))) return os_error("RLIMIT_FSIZE");
+  if (!set_limit(RLIMIT_NOFILE, dict_int(opts, "nofile", 0))) return os_error("RLIMIT_NOFILE");
+
+  // the sandbox's own trees are opened while the process still has the
+  // daemon's identity (a sandbox UID may not be able to walk to them by path)
+  std::vector<int> own_fds, ro_fds;
+  for (auto& p : own_rw) {
+    const int fd = open(p.c_str(), O_PATH | O_CLOEXEC);
+    if (fd >= 0) own_fds.push_back(fd);
+  }
+  for (auto& p : extra_ro) {
+    const int fd = open(p.c_str(), O_PATH | O_CLOEXEC);
+    if (fd >= 0) ro_fds.push_back(fd);
+  }
+  struct Closer {
+    std::vector<int>& a;
+    std::vector<int>& b;
+    ~Closer() {
+      for (int fd : a) close(fd);
+      for (int fd : b) close(fd);
+    }
+  } closer{own_fds, ro_fds};
+
+  // 2. identity: a UID/GID of the sandbox's own (needs CAP_SETUID/CAP_SETGID)
+  if (uid > 0) {
+    if (setgroups(groups.size(), groups.empty() ? nullptr : groups.data()) != 0) return os_error("setgroups");
+    if (setresgid((gid_t)gid, (gid_t)gid, (gid_t)gid) != 0) return os_error("setresgid");
+    // the pids cap is per real UID: set it before switching so it binds
+    if (!set_limit(RLIMIT_NPROC, dict_int(opts, "nproc", 0))) return os_error("RLIMIT_NPROC");
+    if (setresuid((uid_t)uid, (uid_t)uid, (uid_t)uid) != 0) return os_error("setresuid");
+    if (getuid() != (uid_t)uid || geteuid() != (uid_t)uid) {
+      errno = EPERM;
+      return os_error("uid did not change");
+    }
+  }
+  // Sharing the daemon's UID: sibling sandboxes (same UID) must not read this
+  // one's environment or memory through /proc -- non-dumpable (inherited from
+  // the zygote; exec resets it for programs the sandbox starts).  With a UID
+  // of its own, DAC already keeps everyone else out, and the sandbox keeps
+  // normal access to its own /proc/self (the UID switch cleared the flag).
+  prctl(PR_SET_DUMPABLE, uid > 0 ? 1 : 0, 0, 0, 0);
+  // both Landlock and unprivileged seccomp require it; also no setuid
+  // binary or file capability can hand privileges back
+  if (prctl(PR_SET_NO_NEW_PRIVS, 1, 0, 0, 0) != 0) return os_error("PR_SET_NO_NEW_PRIVS");
+
+  // 3. Landlock
+  int abi = want_ll ? ll_abi() : 0;
+  int nrules = 0;
+  uint64_t scoped = 0;
+  if (abi > 0) {
+    const uint64_t fs = handled_fs(abi);
+    RulesetAttr attr{fs, 0, 0};
+    if (abi >= 6) {
+      if (scope_signal) scoped |= kScopeSignal;
+      if (scope_abstract) scoped |= kScopeAbstractUnix;
+      attr.scoped = scoped;
+    }
+    const size_t attr_size = abi >= 6 ? sizeof(RulesetAttr) : abi >= 4 ? 16 : 8;
+    const int rs = (int)syscall(__NR_landlock_create_ruleset, &attr, attr_size, 0);
+    if (rs < 0) return os_error("landlock_create_ruleset");
+    auto add = [&](int fd, uint64_t access) -> bool {
+      landlock_path_beneath_attr pb{};
+      pb.allowed_access = access & fs;
+      pb.parent_fd = fd;
+      if (pb.allowed_access == 0) return true;
+      if (syscall(__NR_landlock_add_rule, rs, LANDLOCK_RULE_PATH_BENEATH, &pb, 0) != 0) {
+        // a rule on a non-directory may only carry file rights
+        pb.allowed_access &= LANDLOCK_ACCESS_FS_EXECUTE | LANDLOCK_ACCESS_FS_WRITE_FILE | LANDLOCK_ACCESS_FS_READ_FILE |
+                             kFsTruncate;
+        if (pb.allowed_access == 0 || syscall(__NR_landlock_add_rule, rs, LANDLOCK_RULE_PATH_BENEATH, &pb, 0) != 0)
+          return false;
+      }
+      ++nrules;
+      return true;
+    };
+    for (auto& r : g_rules) add(r.fd, r.access);
+    for (int fd : own_fds) add(fd, fs);
+    for (int fd : ro_fds) add(fd, kRead);
+    if (syscall(__NR_landlock_restrict_self, rs, 0) != 0) {
+      close(rs);
+      return os_error("landlock_restrict_self");
+    }
+    close(rs);
+  }
+  if (!g_rules.empty()) {
+    // the rule descriptors are the zygote's: not the sandbox's business
+    const int lo = g_rules.front().fd, hi = g_rules.back().fd;
+    if (syscall(SYS_close_range, (unsigned)lo, (unsigned)hi, 0) != 0)
+      for (auto& r : g_rules) close(r.fd);
+    g_rules.clear();
+  }
+
+  if (geteuid() == 0) {
+    // still root (no sandbox UID: layout not walkable by other UIDs, or UID
+    // mode off): shed every capability, so DAC, dumpability and Landlock bind
+    // this process like any unprivileged one.  Under Landlock, CAP_DAC_READ_
+    // SEARCH stays: the view (not DAC) decides what is readable, and root-owned
+    // trees below another user's 0700 $HOME (this package, LD_PRELOAD shims
+    // that exec'd children must load) stay reachable.  It cannot read another
+    // process's /proc entries (that takes CAP_SYS_PTRACE), and
+    // open_by_handle_at is refused by the seccomp filter below.
+    const uint64_t keep = abi > 0 ? (1ULL << CAP_DAC_READ_SEARCH) : 0;
+    for (int c = 0; c <= CAP_LAST_CAP; ++c)
+      if (!((keep >> c) & 1)) prctl(PR_CAPBSET_DROP, c, 0, 0, 0);
+    prctl(PR_CAP_AMBIENT, PR_CAP_AMBIENT_CLEAR_ALL, 0, 0, 0);
+    __user_cap_header_struct hdr{_LINUX_CAPABILITY_VERSION_3, 0};
+    __user_cap_data_struct data[2] = {};
+    data[0].effective = data[0].permitted = (uint32_t)keep;
+    if (syscall(SYS_capset, &hdr, data) != 0) return os_error("capset");
+  }
+
+  // 4. seccomp
+  bool sc = false;
+  if (want_sc && seccomp_available()) {
+    static std::vector<sock_filter> prog = seccomp_program();
+    sock_fprog fp{(unsigned short)prog.size(), prog.data()};
+    if (syscall(SYS_seccomp, SECCOMP_SET_MODE_FILTER, 0, &fp) != 0) return os_error("seccomp");
+    sc = true;
+  }
+  return Py_BuildValue("{s:i,s:i,s:i,s:K,s:O,s:i}", "uid", (int)getuid(), "gid", (int)getgid(), "landlock_abi", abi,
+                       "scoped", (unsigned long long)scoped, "seccomp", sc ? Py_True : Py_False, "landlock_rules",
+                       nrules);
+}
+
+PyObject* py_denied_syscalls(PyObject*, PyObject*) {
+  PyObject* l = PyList_New(0);
+  for (int nr : kDenied) {
+    PyObject* v = PyLong_FromLong(nr);
+    PyList_Append(l, v);
+    Py_DECREF(v);
+  }
+  return l;
+}
+
+PyMethodDef kMethods[] = {
+    {"probe", py_probe, METH_NOARGS, "probe() -> dict: Landlock ABI, seccomp, privilege"},
+    {"prepare", py_prepare, METH_VARARGS, "prepare([(path, access), ...]) -> n: open the static Landlock rules"},
+    {"apply", py_apply, METH_VARARGS, "apply(opts) -> dict: jail the calling (freshly forked) process"},
+    {"denied_syscalls", py_denied_syscalls, METH_NOARGS, "syscall numbers the seccomp filter refuses"},
+    {nullptr, nullptr, 0, nullptr},
+};
+
+PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_jail", "Sandbox isolation: uid drop, Landlock, seccomp, rlimits.", -1,
+                       kMethods};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__jail() {
+  PyObject* m = PyModule_Create(&kModule);
+  if (!m) return nullptr;
+  PyModule_AddIntConstant(m, "READ", (long)kRead);
+  PyModule_AddIntConstant(m, "READ_FILE", (long)LANDLOCK_ACCESS_FS_READ_FILE);
+  PyModule_AddIntConstant(m, "WRITE_FILE", (long)LANDLOCK_ACCESS_FS_WRITE_FILE);
+  PyModule_AddIntConstant(m, "READ_DIR", (long)LANDLOCK_ACCESS_FS_READ_DIR);
+  PyModule_AddIntConstant(m, "TRUNCATE", (long)kFsTruncate);
+  PyModule_AddIntConstant(m, "ALL", (long)(kFsV1 | kFsRefer | kFsTruncate));
+  return m;
+}
