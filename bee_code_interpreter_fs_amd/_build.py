@@ -52,7 +52,9 @@ def _targets() -> List[Target]:
     k = os.path.join(CSRC, "kernels")
     ex = os.path.join(CSRC, "executor")
     q = os.path.join(CSRC, "hbm_quota")
-    ex_srcs = sorted(os.path.join(ex, f) for f in os.listdir(ex) if f.endswith(".cpp")) if os.path.isdir(ex) else []
+    # broker_fuzz.cpp is the CPU fuzz harness's main(), not part of the daemon
+    ex_srcs = sorted(os.path.join(ex, f) for f in os.listdir(ex)
+                     if f.endswith(".cpp") and f != "broker_fuzz.cpp") if os.path.isdir(ex) else []
     ex_hdrs = sorted(os.path.join(ex, f) for f in os.listdir(ex) if f.endswith(".hpp")) if os.path.isdir(ex) else []
     rb = os.path.join(CSRC, "rccl_bench")
     targets = [
@@ -72,7 +74,7 @@ def _targets() -> List[Target]:
             Target(
                 name="bee-executor",
                 output=os.path.join(PKG, "bin", "bee-executor"),
-                sources=sorted(os.path.join(ex, f) for f in os.listdir(ex) if f.endswith(".cpp")),
+                sources=ex_srcs,
                 compiler=CXX,
                 compile_flags=[
                     "-O2", "-g", "-std=c++17", "-Wall", "-Wextra", "-Wno-unused-parameter", "-Wno-unused-result",
@@ -117,6 +119,22 @@ def _targets() -> List[Target]:
                     optional=True,
                 )
             )
+    if ex_srcs:
+        # the broker's protocol core over a host-memory device, under
+        # ASan/UBSan: what tests/test_broker_fuzz_cpu.py drives with hostile frames
+        targets.append(
+            Target(
+                name="broker-fuzz",
+                output=os.path.join(ROOT, "build", "sanitize", "bee-broker-fuzz"),
+                sources=[os.path.join(ex, "broker_core.cpp"), os.path.join(ex, "broker_fuzz.cpp")],
+                compiler=CXX,
+                compile_flags=["-O1", "-g", "-std=c++17", "-Wall", "-Wextra", "-fsanitize=address,undefined",
+                               "-fno-sanitize-recover=all", "-fno-omit-frame-pointer"],
+                link_flags=["-fsanitize=address,undefined", "-static-libasan"],
+                shared=False,
+                headers=[os.path.join(ex, "broker_core.hpp")],
+            )
+        )
     fm = os.path.join(CSRC, "fsmap")
     if os.path.isdir(fm) and os.listdir(fm):
         targets.append(

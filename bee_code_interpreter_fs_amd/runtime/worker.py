@@ -429,7 +429,11 @@ def worker_main(spawn: dict) -> None:
                 from bee_code_interpreter_fs_amd import ops
 
                 if ops.is_initialized() and ops.driver_name() == "native":
-                    ops.set_quota(quota)  # broker sessions are charged by the daemon
+                    ops.set_quota(quota)
+                elif ops.is_initialized() and ops.driver_name() == "broker":
+                    from bee_code_interpreter_fs_amd.ops import array as _ops_array
+
+                    _ops_array.driver().note_quota(quota)  # the daemon charges broker sessions itself
         _redirect_stdio(job["stdout"], job["stderr"])
         _STAMPS["redir"] = time.monotonic() * 1e3
     except BaseException:
