@@ -44,6 +44,7 @@ from .array import (  # noqa: F401
     power,
     random,
     relu,
+    set_lazy_random,
     set_quota,
     sigmoid,
     sin,

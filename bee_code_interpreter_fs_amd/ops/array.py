@@ -570,6 +570,16 @@ def gemm_bf16_tn(a: DeviceArray, bt: DeviceArray, out_dtype: str = "bfloat16", a
 _LAZY_RANDOM = os.environ.get("BEE_LAZY_RANDOM", "1") != "0"
 
 
+def set_lazy_random(enabled: bool) -> bool:
+    """Uniform draws are lazy by default: generated on first use, and fused
+    into a reduction that consumes them directly.  ``False`` materialises
+    every draw in HBM at once (numpy's data movement: the reference
+    payload's 800 MB array).  Returns the previous setting."""
+    global _LAZY_RANDOM
+    prev, _LAZY_RANDOM = _LAZY_RANDOM, bool(enabled)
+    return prev
+
+
 class Generator:
     """Counter-based Philox4x32-10 stream on the device (numpy.random subset)."""
 

@@ -103,9 +103,9 @@ class ExecutorProcess:
         lib = os.path.join(ROOT, "bee_code_interpreter_fs_amd", "ops", "lib", "libbeekern.so")
         if self.broker and self.gpus and os.path.exists(lib):
             cmd += ["--broker-lib", lib]
-        if (self.broker and self.gpus and os.path.exists(lib)) or not self.gpus:
-            # light (torch-free) sandboxes: broker-backed on a GPU, plain on CPU
-            cmd += ["--light-target", str(self.light_target), "--light-zygotes", str(self.light_zygotes)]
+        # light (torch-free) sandboxes: broker-backed on a GPU with a broker,
+        # plain CPU-stack sandboxes otherwise
+        cmd += ["--light-target", str(self.light_target), "--light-zygotes", str(self.light_zygotes)]
         preload = []
         if os.path.exists(fsmap_path()):
             preload.append(fsmap_path())

@@ -36,7 +36,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PAYLOAD = os.path.join(ROOT, "examples", "benchmark_numpy_gpu.py")
+MATERIALIZED = os.path.join(ROOT, "examples", "benchmark_numpy_gpu_materialized.py")
 EXPECTED = 10**8 / 3  # E[sum U^2]
+
+
+def gemm_tolerance(reference: float) -> float:
+    """|checksum - reference| bound: the checksum sums 16.8M bf16-rounded
+    outputs (measured spread of the difference: a few hundred), the
+    reference is exact up to f32 column sums."""
+    return 2000.0 + 1e-3 * abs(reference)
 
 # BASELINE.json configs; "numpy_gpu" is the headline (metric + config the
 # driver records), the others are reported by tools/bench_suite.py.
@@ -85,7 +93,12 @@ def parse_args():
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="numpy_gpu")
     p.add_argument("--payload", default=None, help="override the workload's script")
     p.add_argument("--cpu-only", action="store_true", help="executors without GPUs (BASELINE config 1)")
+    p.add_argument("--virtual-gpus", action="store_true",
+                   help="CPU rehearsal of an N-GPU node: N executors pinned to GPU ids 0..N-1 that need not exist "
+                        "(no kernel broker, no HIP warm-up); use with a CPU workload such as --workload hello")
     p.add_argument("--no-gang-check", action="store_true")
+    p.add_argument("--materialized-steps", type=int, default=-1,
+                   help="steps of the secondary materialised-draw run (numpy's HBM traffic; -1 = min(steps, 20), 0 = skip)")
     return p.parse_args()
 
 
@@ -136,6 +149,14 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def gpu_ids(n_gpus: int, args):
+    """One executor per GPU; a run with more ranks than visible GPUs folds the
+    extra ranks onto the existing devices (and says so in the JSON)."""
+    if args.virtual_gpus:
+        return list(range(n_gpus))
+    return sorted({i % visible_gpus() for i in range(n_gpus)})
+
+
 def start_service(tmp: str, n_gpus: int, args):
     gport, hport = free_port(), free_port()
     frontends = args.frontends or min(8, max(1, n_gpus))
@@ -146,9 +167,7 @@ def start_service(tmp: str, n_gpus: int, args):
             "APP_HTTP_LISTEN_ADDR": f"127.0.0.1:{hport}",
             # one executor per physical GPU (a rehearsal with more ranks than
             # GPUs folds the extra ranks onto the existing devices)
-            "APP_GPU_IDS": json.dumps(sorted({i % visible_gpus() for i in range(n_gpus)}))
-            if not args.cpu_only
-            else "[]",
+            "APP_GPU_IDS": "[]" if args.cpu_only else json.dumps(gpu_ids(n_gpus, args)),
             "APP_FILE_STORAGE_PATH": os.path.join(tmp, "files"),
             "APP_SANDBOX_ROOT": os.path.join(tmp, "sandboxes"),
             "APP_WORKERS_PER_GPU_TARGET": "1",  # direct sandboxes: the payload does not need them
@@ -166,6 +185,8 @@ def start_service(tmp: str, n_gpus: int, args):
             ),
         }
     )
+    if args.virtual_gpus:
+        env.update({"APP_BROKER_ENABLED": "false", "APP_WORKER_WARM_GPU": "false"})
     env.pop("RANK", None), env.pop("WORLD_SIZE", None), env.pop("LOCAL_RANK", None)
     log = open(os.path.join(tmp, "service.log"), "ab")
     proc = subprocess.Popen(
@@ -207,6 +228,10 @@ async def client_loop(target, pb, source, n, out):
             try:
                 if ok and "Result:" in r.stdout:  # benchmark-numpy payloads: check the math
                     ok = abs(float(r.stdout.split("Result:")[1].split()[0]) - EXPECTED) < 5e4
+                if ok and "GEMM reference:" in r.stdout:  # and the GEMM, against the colsum identity
+                    cs = float(r.stdout.split("GEMM checksum:")[1].split()[0])
+                    ref = float(r.stdout.split("GEMM reference:")[1].split()[0])
+                    ok = abs(cs - ref) < gemm_tolerance(ref)
                 if ok and "Execution Time:" in r.stdout:
                     exec_times.append(float(r.stdout.split("Execution Time:")[1].split()[0]) * 1e3)
             except (IndexError, ValueError):
@@ -225,6 +250,51 @@ async def run_clients(targets, first_client, source, concurrency, n):
     await asyncio.gather(
         *(client_loop(targets[(first_client + i) % len(targets)], pb, source, n, out) for i in range(concurrency))
     )
+    return out
+
+
+def _loadgen_main(targets, first, source, concurrency, warmup, steps, barrier, results):
+    """One load-generator process (single-process ``--gpus N`` runs start N
+    of them, so offered load grows with N like the torchrun ranks do)."""
+    sys.path.insert(0, ROOT)
+    loop = asyncio.new_event_loop()
+    try:
+        loop.run_until_complete(run_clients(targets, first, source, concurrency, warmup))
+        barrier.wait()
+        t0 = time.perf_counter()
+        lat, errors, exec_times, phases = loop.run_until_complete(run_clients(targets, first, source, concurrency, steps))
+        results.put((time.perf_counter() - t0, lat, errors, exec_times, phases))
+    except BaseException as e:  # noqa: BLE001 - report instead of hanging the barrier
+        barrier.abort()
+        results.put((0.0, [], [f"loadgen failed: {e!r}"[:300]], [], {}))
+    finally:
+        loop.close()
+
+
+def run_loadgens(n_procs, targets, source, concurrency, warmup, steps, sync, marks=None):
+    """``n_procs`` client processes of ``concurrency`` clients each; times
+    the steps between one barrier all of them (and this process) pass and
+    their completion.  Returns the gathered tuples (elapsed per process)."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    barrier = ctx.Barrier(n_procs + 1)
+    results = ctx.Queue()
+    procs = [ctx.Process(target=_loadgen_main, args=(targets, i * concurrency, source, concurrency, warmup, steps,
+                                                     barrier, results), daemon=True) for i in range(n_procs)]
+    for p in procs:
+        p.start()
+    try:
+        barrier.wait(timeout=900)
+    except Exception:  # a load generator failed during warm-up
+        pass
+    sync()
+    if marks is not None:
+        marks["t0"], marks["cpu0"] = time.perf_counter(), cpu_usage_s()[0]
+    out = [results.get(timeout=3600) for _ in procs]
+    sync()
+    for p in procs:
+        p.join(timeout=30)
     return out
 
 
@@ -260,7 +330,13 @@ def gang_allreduce_check(target, n):
                 pb.ExecuteRequest(source_code=GANG_SCRIPT, gpus=n, timeout=240), timeout=300
             )
         line = [l for l in r.stdout.splitlines() if l.startswith("allreduce_ok")]
-        return {"exit_code": r.exit_code, "result": line[0] if line else None, "stderr_tail": r.stderr[-300:] if r.exit_code else ""}
+        out = {"exit_code": r.exit_code, "result": line[0] if line else None,
+               "stderr_tail": r.stderr[-300:] if r.exit_code else ""}
+        if line:
+            kv = dict(p.split("=", 1) for p in line[0].split())
+            out["ok"] = kv.get("allreduce_ok") == "True"
+            out["busbw_GBps"] = float(kv.get("busbw_GBps", "nan"))
+        return out
     except Exception as e:  # noqa: BLE001
         return {"error": repr(e)[:300]}
 
@@ -319,21 +395,60 @@ def main():
         target = f"127.0.0.1:{gport}"
         targets = replicas or [target]
         first = rank * args.concurrency
+        # offered load: `concurrency` clients per GPU.  torchrun ranks are one
+        # load generator each; a single-process N-GPU run starts N of them.
+        loadgens = n_gpus if world == 1 and n_gpus > 1 else 1
 
-        loop.run_until_complete(run_clients(targets, first, source, args.concurrency, args.warmup))  # warm every pool
-        barrier()
         cpu0, cpu_src = cpu_usage_s()
-        t0 = time.perf_counter()
-        lat, errors, exec_times, phases = loop.run_until_complete(
-            run_clients(targets, first, source, args.concurrency, args.steps))
-        barrier()
-        elapsed = time.perf_counter() - t0
-        cpu_busy = (cpu_usage_s()[0] - cpu0) / elapsed if elapsed > 0 else 0.0
+        if loadgens > 1:
+            marks = {}
+            gathered = run_loadgens(loadgens, targets, source, args.concurrency, args.warmup, args.steps, barrier, marks)
+            elapsed = max(g[0] for g in gathered)
+            cpu_busy = (cpu_usage_s()[0] - marks["cpu0"]) / max(time.perf_counter() - marks["t0"], 1e-9)
+        else:
+            loop.run_until_complete(run_clients(targets, first, source, args.concurrency, args.warmup))  # warm every pool
+            barrier()
+            cpu0, cpu_src = cpu_usage_s()
+            t0 = time.perf_counter()
+            lat, errors, exec_times, phases = loop.run_until_complete(
+                run_clients(targets, first, source, args.concurrency, args.steps))
+            barrier()
+            elapsed = time.perf_counter() - t0
+            cpu_busy = (cpu_usage_s()[0] - cpu0) / elapsed if elapsed > 0 else 0.0
+            gathered = [(elapsed, lat, errors, exec_times, phases)]
+            if world > 1:
+                gathered = [None] * world
+                dist.all_gather_object(gathered, (elapsed, lat, errors, exec_times, phases))
 
-        gathered = [(elapsed, lat, errors, exec_times, phases)]
-        if world > 1:
-            gathered = [None] * world
-            dist.all_gather_object(gathered, (elapsed, lat, errors, exec_times, phases))
+        # secondary: the same payload with every draw materialised in HBM
+        # (the reference's numpy data movement), same clients, untimed by
+        # the headline
+        mat = None
+        mat_steps = args.materialized_steps if args.materialized_steps >= 0 else min(args.steps, 20)
+        if args.workload == "numpy_gpu" and mat_steps > 0 and not args.payload:
+            msrc = open(MATERIALIZED).read()
+            if loadgens > 1:
+                mg = run_loadgens(loadgens, targets, msrc, args.concurrency, 1, mat_steps, barrier)
+            else:
+                loop.run_until_complete(run_clients(targets, first, msrc, args.concurrency, 1))
+                barrier()
+                tm = time.perf_counter()
+                r = loop.run_until_complete(run_clients(targets, first, msrc, args.concurrency, mat_steps))
+                barrier()
+                mg = [(time.perf_counter() - tm,) + tuple(r)]
+                if world > 1:
+                    allmg = [None] * world
+                    dist.all_gather_object(allmg, mg[0])
+                    mg = allmg
+            m_el = max(g[0] for g in mg)
+            m_lat = [x for g in mg for x in g[1]]
+            m_err = [x for g in mg for x in g[2]]
+            mat = {"value": round(len(m_lat) / m_el, 3) if m_el > 0 else 0.0, "steps": mat_steps,
+                   "p50_latency_ms": round(statistics.median(m_lat), 3) if m_lat else None,
+                   "completed": len(m_lat), "errors": len(m_err),
+                   "payload": os.path.relpath(MATERIALIZED, ROOT)}
+            if m_err:
+                mat["first_error"] = m_err[0][:300]
 
         if rank == 0:
             max_elapsed = max(g[0] for g in gathered)
@@ -350,6 +465,9 @@ def main():
                 else None
             )
             total = len(all_lat)
+            clients = args.concurrency * max(world, loadgens)
+            pods = 1 if args.cpu_only else len(gpu_ids(n_gpus, args))
+            kind = "CPU-only" if args.cpu_only else "virtual-GPU (CPU rehearsal)" if args.virtual_gpus else "GPU-pinned"
             out = {
                 "metric": metric,
                 "value": round(total / max_elapsed, 3) if max_elapsed > 0 else 0.0,
@@ -367,10 +485,10 @@ def main():
                 else "synthetic (the payload generates its own inputs)",
                 "config": {
                     "model": model,
-                    "global_batch": args.concurrency * world,
+                    "global_batch": clients,
                     "seq_len": None,
-                    "parallelism": f"{n_gpus} {'CPU-only' if args.cpu_only else 'GPU-pinned'} executor pods, {frontends} front-end replicas, "
-                    f"{args.concurrency * world} concurrent clients"
+                    "parallelism": f"{pods} {kind} executor pods, {frontends} front-end replicas, "
+                    f"{clients} concurrent clients ({args.concurrency} per GPU, {max(world, loadgens)} load-generator processes)"
                     + (f" (round-robin over the {len(replicas)} replica ports)" if replicas else ""),
                     "execution": "every Execute runs in its own single-use sandbox process on the pinned GPU; "
                     "beekern draws are lazy, so sum(square(rand(1e8))) lowers to one fused Philox->square->reduce "
@@ -385,6 +503,10 @@ def main():
             }
             if all_err:
                 out["first_error"] = all_err[0][:400]
+            out["per_gpu_rps"] = round(out["value"] / max(n_gpus, 1), 3)
+            out["gemm_verified"] = args.workload == "numpy_gpu" and not args.payload
+            if mat is not None:
+                out["materialized"] = mat
             if gang is not None:
                 out["gang_allreduce"] = gang
             out["executors"] = executor_stats(hport)

@@ -157,7 +157,10 @@ bool SandboxPool::start(std::string* err) {
   // the zygote is forked+exec'd BEFORE this process touches HIP (broker init)
   const bool want_broker = !cfg_.broker_lib.empty() && !cfg_.gpus.empty() && !cfg_.pod_mode;
   // CPU-only pools use light (torch-free) sandboxes too, just without a broker
-  const bool cpu_light = cfg_.gpus.empty() && !cfg_.pod_mode && cfg_.light_target > 0 && cfg_.light_zygotes > 0;
+  // without a broker (CPU-only pools, or the broker disabled) light
+  // sandboxes are plain CPU-stack sandboxes; one that does reach for the GPU
+  // initialises HIP itself, on its pinned device
+  const bool cpu_light = !want_broker && !cfg_.pod_mode && cfg_.light_target > 0 && cfg_.light_zygotes > 0;
   const int nl = want_broker || cpu_light ? std::max(1, cfg_.light_zygotes) : 0;
   const int nm = nl > 0 && cfg_.min_target > 0 ? cfg_.min_zygotes : 0;
   for (int i = 0; i < 1 + nl + nm; ++i) {

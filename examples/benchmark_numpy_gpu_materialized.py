@@ -1,4 +1,4 @@
-# benchmark-numpy payload, MI355X edition: the reference's workload
+# benchmark-numpy payload, MI355X edition, materialised draws: the reference's workload
 # (examples/benchmark-numpy.py: 1e8 float64 uniform draws, square, sum) on
 # the sandbox's pinned GPU through the hand-written beekern kernels, plus the
 # 4096^3 bf16 GEMM of BASELINE config 3.  Same printed lines as the original,
@@ -9,6 +9,8 @@
 import time
 
 import beekern as bk
+
+bk.set_lazy_random(False)  # materialise every draw in HBM, as numpy does (800 MB for 1e8 f64)
 
 
 def gpu_intensive_computation():

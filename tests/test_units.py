@@ -393,3 +393,26 @@ def test_philox_reference_known_answers():
     assert one((0xFFFFFFFF,) * 4, (0xFFFFFFFF, 0xFFFFFFFF)) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
     assert one((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0)) == [
         0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_job_quota_reaches_a_lazy_broker_session(monkeypatch):
+    """worker._apply_job_quota with a broker-backed (lazy) beekern session:
+    the client learns the run's quota (regression: a name clash with the
+    package's `array` function made every GPU-slot run exit 70)."""
+    import sys
+
+    from bee_code_interpreter_fs_amd import ops
+    from bee_code_interpreter_fs_amd.runtime import worker
+
+    arr = sys.modules["bee_code_interpreter_fs_amd.ops.array"]
+    monkeypatch.setenv("BEE_BROKER_SOCK", "/nonexistent/broker.sock")
+    monkeypatch.setenv("BEE_HBM_QUOTA_BYTES", "0")  # restored after the test
+    monkeypatch.setattr(arr, "_driver", None)
+    ops.init(0, lazy=True)
+    try:
+        worker._apply_job_quota(123 << 20)
+        assert ops.driver_name() == "broker"
+        assert arr.driver().quota == 123 << 20
+        assert os.environ["BEE_HBM_QUOTA_BYTES"] == str(123 << 20)
+    finally:
+        monkeypatch.setattr(arr, "_driver", None)
