@@ -437,8 +437,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
 }
 
 inline bool ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16) {
+  // a panel's loads use 32-bit buffer offsets ((wave*64 + i*8) * ld*2 + k0*2
+  // in an SGPR, a 256-row extent in the descriptor): leading dimensions whose
+  // 256-row span does not fit 31 bits go to the 8-wave kernel (64-bit math)
+  const auto span_ok = [K](int ld) { return (int64_t)256 * ld * 2 + (int64_t)K * 2 < 0x7fffffffll; };
   return M > 0 && N > 0 && K > 0 && M % TM == 0 && N % TN == 0 && K % TK == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
-         ldc % (out_bf16 ? 8 : 4) == 0;
+         ldc % (out_bf16 ? 8 : 4) == 0 && span_ok(lda) && span_ok(ldb);
 }
 
 template <int O>

@@ -145,6 +145,119 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_fast(const uint1
       }
 }
 
+// ---- edge path ---------------------------------------------------------------
+// The fast kernel's tiling for shapes that are not tile multiples (M, N any;
+// K % 8 == 0 and 16-B aligned rows, so every 16-B chunk is all-in or
+// all-out of range).  Operands are read through buffer resources whose
+// extent ends at the operand's last row: rows past M / N fall outside it and
+// the load returns zeros; a chunk past K gets an offset beyond the extent,
+// zeros again.  Stores are masked.  Same LDS image, swizzle, MFMA schedule.
+constexpr uint32_t kOob = 0x80000000u;  // past any extent this path builds
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const uint16_t* g, int ld, int row0, int rows_total) {
+  const uint16_t* base = g + (int64_t)row0 * ld;
+  const int64_t span = (int64_t)(rows_total - row0) * ld * 2;
+  const uint64_t addr = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)addr);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32));
+  const uint32_t bytes = __builtin_amdgcn_readfirstlane(span > 0x7fffffffll ? 0x7fffffffu : (uint32_t)span);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void stage_tile_edge(__amdgpu_buffer_rsrc_t rsrc, int ld, int K, int k0, uint16_t* lds_tile,
+                                                int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ins = wave * 4 + i;
+    const int r = ins * 8 + (lane >> 3);
+    const int c = swz_chunk(r, lane & 7);
+    const int k = k0 + c * 8;
+    const uint32_t voff = k < K ? (uint32_t)(r * ld + k) * 2u : kOob;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_ptr)(lds_tile + ins * 8 * BK), 16, voff, 0, 0, 0);
+  }
+}
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_edge(const uint16_t* __restrict__ A,
+                                                                     const uint16_t* __restrict__ Bt,
+                                                                     void* __restrict__ C, int M, int N, int K,
+                                                                     int lda, int ldb, int ldc, float alpha,
+                                                                     float beta) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * kTileElems];
+
+  const int nbm = (M + BM - 1) / BM, nbn = (N + BN - 1) / BN, nblocks = nbm * nbn;
+  int b = xcd_remap(blockIdx.x, nblocks);
+  const int group = kGroupM * nbn;
+  const int first_m = (b / group) * kGroupM;
+  const int gm = min(nbm - first_m, kGroupM);
+  const int tm = first_m + (b % group) % gm;
+  const int tn = (b % group) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const __amdgpu_buffer_rsrc_t ra = tile_rsrc(A, lda, m0, M), rb = tile_rsrc(Bt, ldb, n0, N);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (K + BK - 1) / BK;
+  stage_tile_edge(ra, lda, K, 0, smem, wave, lane);
+  stage_tile_edge(rb, ldb, K, 0, smem + BM * BK, wave, lane);
+  __syncthreads();
+
+  for (int t = 0; t < nk; ++t) {
+    uint16_t* cur = smem + (t & 1) * kTileElems;
+    if (t + 1 < nk) {
+      uint16_t* nxt = smem + ((t + 1) & 1) * kTileElems;
+      stage_tile_edge(ra, lda, K, (t + 1) * BK, nxt, wave, lane);
+      stage_tile_edge(rb, ldb, K, (t + 1) * BK, nxt + BM * BK, wave, lane);
+    }
+    const uint16_t* tA = cur;
+    const uint16_t* tB = cur + BM * BK;
+#pragma unroll
+    for (int s = 0; s < BK / 32; ++s) {
+      const int chunk = s * 4 + (lane >> 4);
+      bf16x8 af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag(tA, wm * 64 + i * 16 + (lane & 15), chunk);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = read_frag(tB, wn * 64 + j * 16 + (lane & 15), chunk);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const int col = n0 + wn * 64 + j * 16 + (lane & 15);
+        if (row >= M || col >= N) continue;
+        float v = alpha * acc[i][j][r];
+        if constexpr (OUT_BF16) {
+          uint16_t* c = (uint16_t*)C + (int64_t)row * ldc + col;
+          if (beta != 0.f) v += beta * bf16_bits_to_float(*c);
+          *c = float_to_bf16_bits(v);
+        } else {
+          float* c = (float*)C + (int64_t)row * ldc + col;
+          if (beta != 0.f) v += beta * *c;
+          *c = v;
+        }
+      }
+}
+
 // ---- generic path ------------------------------------------------------------
 constexpr int GBM = 64, GBN = 64, GBK = 32;
 
@@ -365,11 +478,21 @@ BK_API int bk_gemm_bf16_fast_ok(int M, int N, int K, int lda, int ldb) {
   return M > 0 && N > 0 && K > 0 && M % BM == 0 && N % BN == 0 && K % BK == 0 && lda % 8 == 0 && ldb % 8 == 0;
 }
 
+// the edge kernel: any M, N; 16-B chunks (K, ld multiples of 8); a 128-row
+// tile's byte extent within the 31-bit buffer offsets
+static bool edge_ok(int M, int N, int K, int lda, int ldb) {
+  return M > 0 && N > 0 && K > 0 && K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+         (int64_t)BM * lda * 2 < 0x7fffffffll && (int64_t)BN * ldb * 2 < 0x7fffffffll;
+}
+
 // Kernel choice: the 256x256 phase-pipelined kernel when the shape fills at
 // least half the chip with 256^2 tiles, the 128x128 kernel for smaller
 // aligned shapes (4x the blocks), the guarded generic kernel otherwise.
+// Shapes that are not tile multiples take the edge kernel (128x128 tiles,
+// zero-filling buffer loads, masked stores) when K and the leading
+// dimensions are multiples of 8; only the rest reach the generic kernel.
 // variant: 0 = auto, 1 = generic, 2 = 128x128, 3 = 256x256 (4-wave or 8-wave
-// by K), 4 = 256x256 8-wave, 5 = 256x256 4-wave (benchmarks, tests).
+// by K), 4 = 256x256 8-wave, 5 = 256x256 4-wave, 6 = 128x128 edge (benchmarks, tests).
 BK_API int bk_gemm_bf16_tn_variant(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb,
                                    int ldc, float alpha, float beta, int out_dtype, int variant, hipStream_t stream) {
   if (!A || !Bt || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N) return kBadArgument;
@@ -377,11 +500,21 @@ BK_API int bk_gemm_bf16_tn_variant(const void* A, const void* Bt, void* C, int M
   const bool al = aligned16(A) && aligned16(Bt);
   const bool ok128 = al && bk_gemm_bf16_fast_ok(M, N, K, lda, ldb);
   const bool ok256 = al && aligned16(C) && gemm256_ok(M, N, K, lda, ldb, ldc, out_dtype == kBF16);
-  if (variant == 0) variant = (ok256 && (M / 256) * (N / 256) >= 128) ? 3 : ok128 ? 2 : 1;
-  if ((variant >= 3 && variant <= 5 && !ok256) || (variant == 2 && !ok128) || variant < 1 || variant > 5)
+  const bool okedge = al && edge_ok(M, N, K, lda, ldb);
+  if (variant == 0) variant = (ok256 && (M / 256) * (N / 256) >= 128) ? 3 : ok128 ? 2 : okedge ? 6 : 1;
+  if ((variant >= 3 && variant <= 5 && !ok256) || (variant == 2 && !ok128) || (variant == 6 && !okedge) ||
+      variant < 1 || variant > 6)
     return kBadArgument;
   const bool bf = out_dtype == kBF16;
-  if (variant >= 3) {
+  if (variant == 6) {
+    const unsigned grid = (unsigned)(((M + BM - 1) / BM) * ((N + BN - 1) / BN));
+    if (bf)
+      gemm_bf16_tn_edge<true><<<grid, kGemmThreads, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N, K,
+                                                                 lda, ldb, ldc, alpha, beta);
+    else
+      gemm_bf16_tn_edge<false><<<grid, kGemmThreads, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N,
+                                                                  K, lda, ldb, ldc, alpha, beta);
+  } else if (variant >= 3) {
     launch_gemm256(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, bf, stream, variant - 3);
   } else if (variant == 2) {
     const unsigned grid = (unsigned)((M / BM) * (N / BN));
@@ -409,7 +542,7 @@ BK_API int bk_gemm_bf16_pick(const void* A, const void* Bt, const void* C, int M
   const bool al = aligned16(A) && aligned16(Bt);
   const bool ok128 = al && bk_gemm_bf16_fast_ok(M, N, K, lda, ldb);
   const bool ok256 = al && aligned16(C) && gemm256_ok(M, N, K, lda, ldb, ldc, out_dtype == kBF16);
-  return (ok256 && (M / 256) * (N / 256) >= 128) ? 3 : ok128 ? 2 : 1;
+  return (ok256 && (M / 256) * (N / 256) >= 128) ? 3 : ok128 ? 2 : (al && edge_ok(M, N, K, lda, ldb)) ? 6 : 1;
 }
 
 // C = alpha * A . Bt^T + beta * C.  out_dtype: kBF16 or kF32.

@@ -326,7 +326,66 @@ def test_torch_interop(gpu):
     torch.testing.assert_close(back, t * t)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("shape", [(1000, 1000, 1000), (511, 769, 328), (4095, 4097, 4096), (130, 1, 8)])
+@pytest.mark.parametrize("out", ["float32", "bfloat16"])
+def test_gemm_edge_kernel_unaligned_shapes(gpu, shape, out):
+    """The MFMA edge kernel (variant 6, what `auto` picks for non-tile
+    shapes with K % 8 == 0): zero-filled buffer loads past M / N / K, masked
+    stores -- against fp64, beta epilogue included, C's padding untouched."""
+    import torch
+
+    from bee_code_interpreter_fs_amd.ops import _native
+
+    M, N, K = shape
+    ldc = N + 8
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    bt = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    dt = torch.float32 if out == "float32" else torch.bfloat16
+    c0 = torch.empty(M, ldc, device="cuda", dtype=dt).uniform_(-1, 1, generator=g)
+    c = c0.clone()
+    lib = _native.lib()
+    assert lib.bk_gemm_bf16_pick(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, ldc,
+                                 0 if out == "float32" else 2) == 6
+    rc = lib.bk_gemm_bf16_tn_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, ldc, 0.75, 0.5,
+                                     0 if out == "float32" else 2, 0, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = 0.75 * (a.double() @ bt.double().T) + 0.5 * c0[:, :N].double()
+    tol = 1e-3 if out == "float32" else 4e-2
+    assert (c[:, :N].double() - ref).abs().max().item() < tol * max(1.0, ref.abs().max().item())
+    assert torch.equal(c[:, N:], c0[:, N:])  # masked stores: the padding columns are intact
+
+
+def test_gemm_huge_leading_dimension(gpu):
+    """lda > 4.4M: the 4-wave kernel's 32-bit buffer offsets would wrap; the
+    dispatcher must route such operands to 64-bit addressing (round-1
+    review, weak #3).  A is a 256 x 256 window of rows 4.5M elements apart."""
+    import torch
+
+    from bee_code_interpreter_fs_amd.ops import _native
+
+    M = N = 256
+    K = 256
+    lda = 4_500_000
+    g = torch.Generator(device="cuda").manual_seed(5)
+    store = torch.empty(M * lda, device="cuda", dtype=torch.bfloat16)  # 2.3 GB
+    a = store.view(M, lda)[:, :K]
+    a.uniform_(-1, 1, generator=g)
+    bt = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    ref = a.double() @ bt.double().T
+    lib = _native.lib()
+    for variant in (0, 3, 5):
+        c = torch.zeros(M, N, device="cuda", dtype=torch.float32)
+        rc = lib.bk_gemm_bf16_tn_variant(store.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, lda, K, N, 1.0, 0.0, 0,
+                                         variant, torch.cuda.current_stream().cuda_stream)
+        assert rc == 0, variant
+        torch.cuda.synchronize()
+        assert (c.double() - ref).abs().max().item() < 1e-3 * max(1.0, ref.abs().max().item()), variant
+    del store
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("out", ["float32", "bfloat16"])
 def test_gemm_kernel_variants_with_beta(gpu, variant, out):
     """Every GEMM kernel (generic / 128^2 / 256^2 by shape / 256^2 8-wave
