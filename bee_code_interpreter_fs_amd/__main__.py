@@ -98,6 +98,22 @@ async def main() -> None:
         await ctx.close()
 
 
+def _pin_replica(config: Config, backend, index: int, pid: int) -> None:
+    """Replica i runs next to GPU slot i (mod the slot count): its CPU work
+    is mostly that slot's sandboxes' RPCs."""
+    if (config.numa_affinity or "auto").lower() == "off" or not getattr(backend, "slots", None):
+        return
+    from .scheduler.topology import slot_cpus
+
+    slot = backend.slots[index % len(backend.slots)]
+    cpus = slot_cpus(slot.gpu)
+    if cpus:
+        try:
+            os.sched_setaffinity(pid, cpus)
+        except OSError:
+            pass
+
+
 async def supervise(config: Config, n_frontends: int) -> None:
     """Own the executors; run front-end replicas as child processes."""
     ctx = ApplicationContext(config)
@@ -122,6 +138,7 @@ async def supervise(config: Config, n_frontends: int) -> None:
     for i in range(n_frontends):
         e = dict(env, BEE_FRONTEND_INDEX=str(i))
         children.append(subprocess.Popen([sys.executable, "-m", "bee_code_interpreter_fs_amd"], env=e, stdout=subprocess.PIPE))
+        _pin_replica(config, backend, i, children[-1].pid)
     loop = asyncio.get_running_loop()
     replicas = []
     for c in children:  # wait until every replica serves
@@ -149,6 +166,7 @@ async def supervise(config: Config, n_frontends: int) -> None:
                     children[i] = subprocess.Popen(
                         [sys.executable, "-m", "bee_code_interpreter_fs_amd"], env=e, stdout=subprocess.DEVNULL
                     )
+                    _pin_replica(config, backend, i, children[i].pid)
     finally:
         for c in children:
             if c.poll() is None:

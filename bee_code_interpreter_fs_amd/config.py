@@ -146,6 +146,13 @@ class Config:
     # UID 1001050000 (executor/Dockerfile:91-98).
     sandbox_uid_base: int = 1001050000
     sandbox_uid_count: int = 4096
+    # pin each GPU slot's executor (and what it forks) and each front-end
+    # replica to the CPUs of its GPU's NUMA node: "auto" (when the GPUs span
+    # several NUMA nodes) or "off"
+    numa_affinity: str = "auto"
+    # a gang whose rank failed: seconds the other ranks get to finish before
+    # the whole gang is killed (they are usually stuck in a collective)
+    gang_failure_grace_s: float = 10.0
     # processes per sandbox (RLIMIT_NPROC of its UID; UID mode)
     sandbox_max_processes: int = 1024
     # private writable memory per sandbox process without a HIP runtime

@@ -67,10 +67,11 @@ def busbw_budget_gbps(world: int) -> float:
 
 
 def rccl_allreduce_sweep(
-    gpus: Optional[int] = None, min_bytes: str = "1K", max_bytes: str = "1G", iters: int = 20, timeout: float = 600
+    gpus: Optional[int] = None, min_bytes: str = "1K", max_bytes: str = "1G", iters: int = 20, timeout: float = 600,
+    dtype: str = "f32",
 ) -> List[dict]:
-    """Run ``bee-rccl-bench`` and return its JSON records."""
-    cmd = [RCCL_BENCH, "--min", str(min_bytes), "--max", str(max_bytes), "--iters", str(iters)]
+    """Run ``bee-rccl-bench`` (``dtype`` f32 or bf16) and return its JSON records."""
+    cmd = [RCCL_BENCH, "--min", str(min_bytes), "--max", str(max_bytes), "--iters", str(iters), "--dtype", dtype]
     if gpus:
         cmd += ["--gpus", str(gpus)]
     proc = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)

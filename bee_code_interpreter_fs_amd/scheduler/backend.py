@@ -15,7 +15,7 @@ import abc
 from dataclasses import dataclass, field
 from typing import Dict, List, Mapping, Optional
 
-from ..utils.validation import ValidationError, check_absolute_path, check_file_map
+from ..utils.validation import ValidationError, check_absolute_path, check_env, check_file_map
 
 
 @dataclass
@@ -55,6 +55,7 @@ class ExecuteRequest:
             raise ValidationError("nprocs must be 1 or equal to gpus")
         if self.hbm_bytes is not None and int(self.hbm_bytes) < 0:
             raise ValidationError("hbm_bytes must be >= 0")
+        self.env = check_env(self.env)
         return self
 
 

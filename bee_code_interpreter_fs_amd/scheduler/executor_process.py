@@ -58,8 +58,10 @@ class ExecutorProcess:
         broker: bool = False,
         light_zygotes: int = 2,
         extra_args: Optional[List[str]] = None,
+        cpus: Optional[List[int]] = None,
     ) -> None:
         self.extra_args = list(extra_args or [])
+        self.cpus = list(cpus or [])
         self.light_target = light_target
         self.light_zygotes = light_zygotes
         self.broker = broker
@@ -114,6 +116,10 @@ class ExecutorProcess:
             preload.append(interposer)
         if preload:
             cmd += ["--preload", ":".join(preload)]
+        if self.cpus:
+            from .topology import format_cpulist
+
+            cmd += ["--cpus", format_cpulist(self.cpus)]
         return cmd + self.extra_args
 
     async def start(self, timeout: float = 60.0) -> None:

@@ -37,6 +37,7 @@ from ..config import Config
 from ..services.storage import Storage
 from .backend import CodeExecutor, ExecuteRequest, ExecutionResult
 from .executor_process import ExecutorProcess
+from .topology import slot_cpus
 from .uds_http import UdsHttpError
 
 logger = logging.getLogger("local_gpu_pool")
@@ -163,9 +164,11 @@ class LocalGpuPoolBackend(CodeExecutor):
             light_target=c.light_workers_per_gpu_target,
             broker=c.broker_enabled,
             light_zygotes=c.light_zygotes_per_gpu,
+            cpus=slot_cpus(gpu) if (c.numa_affinity or "auto").lower() != "off" else None,
             extra_args=["--max-idle", str(c.worker_max_idle_s), "--min-target", str(c.min_workers_per_gpu_target),
                         "--min-zygotes", str(c.min_zygotes_per_gpu),
                         "--min-cpu-target", str(c.min_cpu_workers_per_gpu_target),
+                        "--gang-grace", str(c.gang_failure_grace_s),
                         *isolation_args(c, i, [self.storage.storage_path])],
         )
 

@@ -36,10 +36,24 @@
     }                                                                                          \
   } while (0)
 
-__global__ void fill_kernel(float* p, size_t n, float v) {
+template <typename T>
+__global__ void fill_kernel(T* p, size_t n, T v) {
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   size_t stride = (size_t)gridDim.x * blockDim.x;
   for (; i < n; i += stride) p[i] = v;
+}
+
+// bf16 bits of a small integer-valued float (exact for the checks here)
+static uint16_t to_bf16(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return (uint16_t)((u + 0x7fff + ((u >> 16) & 1)) >> 16);
+}
+static float from_bf16(uint16_t b) {
+  uint32_t u = (uint32_t)b << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
 }
 
 static int64_t parse_size(const char* s) {
@@ -56,13 +70,26 @@ int main(int argc, char** argv) {
   HIPCHECK(hipGetDeviceCount(&ngpus));
   int64_t min_bytes = 1 << 10, max_bytes = 1LL << 30;
   int iters = 20;
+  std::string dtype = "f32";
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a == "--gpus" && i + 1 < argc) ngpus = std::min(ngpus, atoi(argv[++i]));
     else if (a == "--min" && i + 1 < argc) min_bytes = parse_size(argv[++i]);
     else if (a == "--max" && i + 1 < argc) max_bytes = parse_size(argv[++i]);
     else if (a == "--iters" && i + 1 < argc) iters = atoi(argv[++i]);
+    else if (a == "--dtype" && i + 1 < argc) dtype = argv[++i];
+    else {
+      fprintf(stderr, "usage: bee-rccl-bench [--gpus N] [--min BYTES] [--max BYTES] [--iters K] [--dtype f32|bf16]\n");
+      return 1;
+    }
   }
+  if (dtype != "f32" && dtype != "bf16") {
+    fprintf(stderr, "--dtype must be f32 or bf16\n");
+    return 1;
+  }
+  const bool bf16 = dtype == "bf16";
+  const size_t es = bf16 ? 2 : 4;
+  const ncclDataType_t nt = bf16 ? ncclBfloat16 : ncclFloat;
   if (ngpus < 1) {
     fprintf(stderr, "no GPUs\n");
     return 1;
@@ -72,26 +99,32 @@ int main(int argc, char** argv) {
   std::vector<ncclComm_t> comms(ngpus);
   NCCLCHECK(ncclCommInitAll(comms.data(), ngpus, devs.data()));
   std::vector<hipStream_t> streams(ngpus);
-  std::vector<float*> buf(ngpus);
-  const size_t max_count = (size_t)(max_bytes / 4);
+  std::vector<void*> buf(ngpus);
+  const size_t max_count = (size_t)(max_bytes / es);
   for (int i = 0; i < ngpus; ++i) {
     HIPCHECK(hipSetDevice(i));
     HIPCHECK(hipStreamCreateWithFlags(&streams[i], hipStreamNonBlocking));
-    HIPCHECK(hipMalloc(&buf[i], max_count * sizeof(float)));
+    HIPCHECK(hipMalloc(&buf[i], max_count * es));
   }
-  printf("{\"tool\": \"bee-rccl-bench\", \"gpus\": %d, \"rccl_version\": %d}\n", ngpus, NCCL_VERSION_CODE);
+  printf("{\"tool\": \"bee-rccl-bench\", \"gpus\": %d, \"dtype\": \"%s\", \"rccl_version\": %d}\n", ngpus,
+         dtype.c_str(), NCCL_VERSION_CODE);
   bool all_ok = true;
   for (int64_t bytes = min_bytes; bytes <= max_bytes; bytes *= 2) {
-    const size_t count = (size_t)(bytes / 4);
+    const size_t count = (size_t)(bytes / es);
     for (int i = 0; i < ngpus; ++i) {
       HIPCHECK(hipSetDevice(i));
-      hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, streams[i], buf[i], count, (float)(i + 1));
+      if (bf16)
+        hipLaunchKernelGGL(fill_kernel<uint16_t>, dim3(1024), dim3(256), 0, streams[i], (uint16_t*)buf[i], count,
+                           to_bf16((float)(i + 1)));
+      else
+        hipLaunchKernelGGL(fill_kernel<float>, dim3(1024), dim3(256), 0, streams[i], (float*)buf[i], count,
+                           (float)(i + 1));
     }
     auto run = [&](int k) {
       for (int it = 0; it < k; ++it) {
         NCCLCHECK(ncclGroupStart());
         for (int i = 0; i < ngpus; ++i)
-          NCCLCHECK(ncclAllReduce(buf[i], buf[i], count, ncclFloat, ncclSum, comms[i], streams[i]));
+          NCCLCHECK(ncclAllReduce(buf[i], buf[i], count, nt, ncclSum, comms[i], streams[i]));
         NCCLCHECK(ncclGroupEnd());
       }
       for (int i = 0; i < ngpus; ++i) {
@@ -102,11 +135,22 @@ int main(int argc, char** argv) {
     run(1);  // correctness: every element = n(n+1)/2
     bool ok = true;
     if (bytes == min_bytes || bytes * 2 > max_bytes) {
-      std::vector<float> host(std::min<size_t>(count, 4096));
+      const size_t nh = std::min<size_t>(count, 4096);
+      std::vector<char> host(nh * es);
       HIPCHECK(hipSetDevice(ngpus - 1));
-      HIPCHECK(hipMemcpy(host.data(), buf[ngpus - 1], host.size() * 4, hipMemcpyDeviceToHost));
+      HIPCHECK(hipMemcpy(host.data(), buf[ngpus - 1], host.size(), hipMemcpyDeviceToHost));
       const float want = ngpus * (ngpus + 1) / 2.0f;
-      for (float v : host) ok = ok && v == want;
+      for (size_t k = 0; k < nh; ++k) {
+        float v;
+        if (bf16) {
+          uint16_t b;
+          memcpy(&b, host.data() + k * 2, 2);
+          v = from_bf16(b);
+        } else {
+          memcpy(&v, host.data() + k * 4, 4);
+        }
+        ok = ok && v == want;
+      }
       all_ok = all_ok && ok;
     }
     run(2);  // warm

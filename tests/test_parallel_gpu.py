@@ -1,15 +1,31 @@
-"""RCCL on the GPU box: native all-reduce sweep + a gang sandbox job."""
+"""RCCL on the GPU box: the native all-reduce sweep at every power-of-two
+GPU count the box shows (1 on the per-round box; 2/4/8 on a full node), in
+f32 and bf16, correctness-checked by the tool, with a bus-bandwidth floor
+for multi-GPU counts."""
 
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
-def test_native_rccl_allreduce_sweep():
-    from bee_code_interpreter_fs_amd.parallel import rccl_allreduce_sweep
+def _counts():
+    import torch
 
-    recs = rccl_allreduce_sweep(min_bytes="4K", max_bytes="64M", iters=5)
-    head, rows = recs[0], recs[1:]
-    assert head["gpus"] >= 1
-    assert rows and all(r["checked"] for r in rows)
-    assert rows[-1]["bytes"] == 64 << 20
+    n = torch.cuda.device_count()
+    return [c for c in (1, 2, 4, 8) if c <= n] or [1]
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_native_rccl_allreduce_sweep(dtype):
+    from bee_code_interpreter_fs_amd.parallel import busbw_budget_gbps, rccl_allreduce_sweep
+
+    for n in _counts():
+        recs = rccl_allreduce_sweep(gpus=n, min_bytes="4K", max_bytes="256M", iters=5, dtype=dtype)
+        head, rows = recs[0], recs[1:]
+        assert head["gpus"] == n and head["dtype"] == dtype
+        assert rows and all(r["checked"] for r in rows), rows
+        assert rows[-1]["bytes"] == 256 << 20
+        if n > 1:
+            # xGMI: a ring all-reduce of 256 MB should move well beyond one
+            # link's worth per GPU; and nothing can beat all 7 links
+            assert 50.0 < rows[-1]["busbw_GBps"] < busbw_budget_gbps(n) * 1.05, rows[-1]

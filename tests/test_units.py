@@ -416,3 +416,60 @@ def test_job_quota_reaches_a_lazy_broker_session(monkeypatch):
         assert os.environ["BEE_HBM_QUOTA_BYTES"] == str(123 << 20)
     finally:
         monkeypatch.setattr(arr, "_driver", None)
+
+
+def test_request_env_allow_list():
+    """Gang / custom env: RCCL and torch knobs pass, anything that could
+    steer the sandbox bootstrap (jail, quota, pin, loader) is refused."""
+    from bee_code_interpreter_fs_amd.scheduler.backend import ExecuteRequest
+    from bee_code_interpreter_fs_amd.utils.validation import ValidationError
+
+    ok = ExecuteRequest(source_code="x", env={"NCCL_MIN_NCHANNELS": "16", "RCCL_MSCCL_ENABLE": "0",
+                                              "TORCH_NCCL_ASYNC_ERROR_HANDLING": "1", "OMP_NUM_THREADS": "4"}).validate()
+    assert ok.env["NCCL_MIN_NCHANNELS"] == "16"
+    for bad in ({"BEE_JAIL": "0"}, {"LD_PRELOAD": "/x.so"}, {"HIP_VISIBLE_DEVICES": "0,1"}, {"PYTHONPATH": "/x"},
+                {"BEE_HBM_QUOTA_BYTES": "0"}, {"A=B": "1"}, {"HSA_TOOLS_LIB": "x"}):
+        with pytest.raises(ValidationError):
+            ExecuteRequest(source_code="x", env=bad).validate()
+
+
+def _fake_sysfs(root, gpus_numa):
+    """KFD topology (one CPU node, then GPU nodes) + PCI numa_node + node cpulists."""
+    import os
+
+    base = os.path.join(root, "class", "kfd", "kfd", "topology", "nodes")
+    os.makedirs(os.path.join(base, "0"))
+    open(os.path.join(base, "0", "properties"), "w").write("cpu_cores_count 64\nsimd_count 0\n")
+    for i, numa in enumerate(gpus_numa):
+        d = os.path.join(base, str(i + 1))
+        os.makedirs(d)
+        bus = 0x10 + 0x10 * i
+        open(os.path.join(d, "properties"), "w").write(f"simd_count 1024\nlocation_id {bus << 8}\ndomain 0\n")
+        pci = os.path.join(root, "bus", "pci", "devices", f"0000:{bus:02x}:00.0")
+        os.makedirs(pci)
+        open(os.path.join(pci, "numa_node"), "w").write(f"{numa}\n")
+    for node, cpus in ((0, "0-3,8-11"), (1, "4-7,12-15")):
+        d = os.path.join(root, "devices", "system", "node", f"node{node}")
+        os.makedirs(d)
+        open(os.path.join(d, "cpulist"), "w").write(cpus + "\n")
+
+
+def test_numa_topology_and_slot_cpus(tmp_path):
+    from bee_code_interpreter_fs_amd.scheduler import topology as t
+
+    assert t.parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+    assert t.format_cpulist([11, 10, 8, 3, 2, 1, 0]) == "0-3,8,10-11"
+    _fake_sysfs(str(tmp_path), [0, 0, 0, 0, 1, 1, 1, 1])
+    assert t.gpu_numa_nodes(str(tmp_path)) == [0, 0, 0, 0, 1, 1, 1, 1]
+    assert t.slot_cpus(0, str(tmp_path), allowed=set(range(16))) == [0, 1, 2, 3, 8, 9, 10, 11]
+    assert t.slot_cpus(6, str(tmp_path), allowed=set(range(16))) == [4, 5, 6, 7, 12, 13, 14, 15]
+    assert t.slot_cpus(6, str(tmp_path), allowed={0, 1, 5}) == [5]  # only CPUs this process may use
+    assert t.slot_cpus(None, str(tmp_path)) == []
+
+
+def test_numa_single_node_means_no_pinning(tmp_path):
+    from bee_code_interpreter_fs_amd.scheduler import topology as t
+
+    _fake_sysfs(str(tmp_path), [0, 0])
+    assert t.slot_cpus(1, str(tmp_path), allowed=set(range(16))) == []
+    assert t.gpu_numa_nodes(str(tmp_path / "missing")) == []
