@@ -54,7 +54,8 @@ void usage() {
           "                    [--min-target N] [--min-zygotes N] [--min-preload MODS] [--min-cpu-target N]\n"
           "                    [--workspace DIR] [--runtime-packages DIR] [--die-with-parent 0|1]\n"
           "                    [--jail 0|1] [--uid-base UID] [--uid-count N] [--protect DIR]... [--nproc N]\n"
-          "                    [--mem-limit BYTES] [--cpus LIST] [--gang-grace S]\n");
+          "                    [--mem-limit BYTES] [--cpus LIST] [--gang-grace S]\n"
+          "                    [--hbm-watchdog-ms MS] [--hbm-slack BYTES]\n");
 }
 
 bool resolve_pod_path(const PoolConfig& cfg, const std::string& url_path, std::string* real, std::string* err) {
@@ -138,6 +139,8 @@ int main(int argc, char** argv) {
     else if (a == "--nproc") cfg.nproc = atoll(val().c_str());
     else if (a == "--mem-limit") cfg.mem_bytes = atoll(val().c_str());
     else if (a == "--gang-grace") cfg.gang_grace_s = atof(val().c_str());
+    else if (a == "--hbm-watchdog-ms") cfg.hbm_watchdog_ms = atoi(val().c_str());
+    else if (a == "--hbm-slack") cfg.hbm_slack = atoll(val().c_str());
     else if (a == "-h" || a == "--help") {
       usage();
       return 0;
