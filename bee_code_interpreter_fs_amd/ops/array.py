@@ -251,11 +251,11 @@ class DeviceArray:
     def copy(self) -> "DeviceArray":
         return _unary("copy", self)
 
-    def sum(self):
-        return sum(self)
+    def sum(self, axis: Optional[int] = None):
+        return sum(self, axis)
 
-    def mean(self):
-        return sum(self) / self.size
+    def mean(self, axis: Optional[int] = None):
+        return mean(self, axis)
 
     def max(self):
         return _reduce("max", self)
@@ -442,8 +442,33 @@ def _rand_reduce(op: str, x: DeviceArray) -> np.float64:
     return np.float64(driver().rand_reduce(_REDUCE[op], x.code, x.size, seed, off, lo, hi))
 
 
-def sum(x) -> np.float64:  # noqa: A001 - numpy-compatible name
+def _reduce_axis(op: str, x: DeviceArray, axis: int):
+    """sum / mean of a 2-D array along ``axis`` (numpy semantics: axis 0
+    collapses the rows -> one value per column).  f64 in -> f64 out; f32 and
+    bf16 in -> f32 out; f64 accumulation (bk_reduce_axis)."""
+    if x.ndim == 1:
+        if axis not in (0, -1):
+            raise ValueError(f"axis {axis} is out of bounds for a 1-D array")
+        return sum(x) if op == "sum" else mean(x)  # numpy: a scalar
+    if x.ndim != 2:
+        raise ValueError("axis reductions support 1-D and 2-D arrays")
+    axis = axis + 2 if axis < 0 else axis
+    if axis not in (0, 1):
+        raise ValueError(f"axis {axis} is out of bounds for a 2-D array")
+    if x._lazy is not None:
+        x._materialize()
+    rows, cols = x.shape
+    if x._transposed:  # a .T view: the buffer is (cols, rows) -- reduce the other way
+        rows, cols, axis = cols, rows, 1 - axis
+    out = DeviceArray((cols if axis == 0 else rows,), "float64" if x.dtype == "float64" else "float32")
+    driver().reduce_axis(0 if op == "sum" else 1, x.code, x._buf.ptr, out.ptr, rows, cols, cols, axis)  # type: ignore[union-attr]
+    return out
+
+
+def sum(x, axis: Optional[int] = None):  # noqa: A001 - numpy-compatible name
     x = _as_operand(x)
+    if axis is not None:
+        return _reduce_axis("sum", x, int(axis))
     if x._lazy is not None and x._lazy[0] == "square":
         base = x._lazy[1]
         if _lazy_uniform(base):
@@ -461,8 +486,10 @@ def square_sum(x) -> np.float64:
     return _reduce("square_sum", x._materialize())
 
 
-def mean(x) -> np.float64:
+def mean(x, axis: Optional[int] = None):
     x = _as_operand(x)
+    if axis is not None:
+        return _reduce_axis("mean", x, int(axis))
     return sum(x) / x.size
 
 

@@ -41,6 +41,7 @@ class NativeDriver:
         self.device: Optional[int] = None
         self.ws = 0
         self.scalar = 0
+        self.axis_ws = 0
 
     def init(self, device: int) -> None:
         check(self.lib.bk_init(int(device)), "bk_init")
@@ -98,6 +99,12 @@ class NativeDriver:
             self.lib.bk_gemm_bf16_tn(_vp(A), _vp(Bt), _vp(C), M, N, K, lda, ldb, ldc, alpha, beta, odt, self.stream),
             "bk_gemm_bf16_tn",
         )
+
+    def reduce_axis(self, op: int, dt: int, x: int, y: int, rows: int, cols: int, ld: int, axis: int) -> None:
+        if not self.axis_ws:
+            self.axis_ws = self.malloc(self.lib.bk_reduce_axis_workspace_bytes())
+        check(self.lib.bk_reduce_axis(op, dt, _vp(x), rows, cols, ld, axis, _vp(y), _vp(self.axis_ws), self.stream),
+              "bk_reduce_axis")
 
     def transpose(self, src: int, dst: int, rows: int, cols: int, ldi: int, ldo: int, src_dtype: int = 2,
                   dst_dtype: int = 2) -> None:
@@ -157,7 +164,7 @@ def _info_dict(v, arch: str) -> dict:
 # ---- broker client --------------------------------------------------------------------
 
 (HELLO, ALLOC, FREE, WRITE, READ, RAND, UNARY, BINARY, CAST, FILL, REDUCE, GEMM, TRANSPOSE, SYNC, MEMSTATS, INFO,
- COPY, RAND_REDUCE, ALLOC_AT) = range(1, 20)
+ COPY, RAND_REDUCE, ALLOC_AT, REDUCE_AXIS) = range(1, 21)
 _HDR = struct.Struct("<IIQ")
 _NO_REPLY = 1  # request flag: no response unless a later request collects an error
 _RHDR = struct.Struct("<iIQ")
@@ -314,6 +321,9 @@ class BrokerDriver:
 
     def gemm(self, A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt) -> None:
         self._post(GEMM, struct.pack("<QQQiiiiiiffii", A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, 0))
+
+    def reduce_axis(self, op, dt, x, y, rows, cols, ld, axis) -> None:
+        self._post(REDUCE_AXIS, struct.pack("<IIQQqqqII", op, dt, x, y, rows, cols, ld, axis, 0))
 
     def transpose(self, src, dst, rows, cols, ldi, ldo, src_dtype=2, dst_dtype=2) -> None:
         self._post(TRANSPOSE, struct.pack("<QQiiiiii", src, dst, rows, cols, ldi, ldo, src_dtype, dst_dtype))

@@ -80,6 +80,8 @@ class HipDevice final : public broker::Device {
     int (*gemm)(const void*, const void*, void*, int, int, int, int, int, int, float, float, int, hipStream_t);
     int (*transpose)(int, int, const void*, void*, int, int, int, int, hipStream_t);
     int (*preload)(hipStream_t);
+    int64_t (*axis_ws)();
+    int (*reduce_axis)(int, int, const void*, int64_t, int64_t, int64_t, int, void*, void*, hipStream_t);
   } bk{};
 
   // Per-session GPU resources, pooled across sessions: a stream, the
@@ -91,6 +93,7 @@ class HipDevice final : public broker::Device {
     void* ws = nullptr;
     void* scalar = nullptr;  // device fallback when no pinned slot exists
     double* slot = nullptr;
+    void* axis_ws = nullptr;  // axis-reduction partials, allocated on first use
   };
 
   bool load(const std::string& path, std::string* err) {
@@ -112,6 +115,8 @@ class HipDevice final : public broker::Device {
       return false;
     }
     sym(lib_, "bk_preload", &bk.preload);
+    sym(lib_, "bk_reduce_axis_workspace_bytes", &bk.axis_ws);
+    sym(lib_, "bk_reduce_axis", &bk.reduce_axis);
     return true;
   }
 
@@ -230,6 +235,13 @@ class HipDevice final : public broker::Device {
   }
   int transpose(int sdt, int ddt, const void* in, void* out, int rows, int cols, int ldi, int ldo, void* s) override {
     return bk.transpose(sdt, ddt, in, out, rows, cols, ldi, ldo, st(s));
+  }
+  int reduce_axis(uint32_t op, uint32_t dt, const void* x, void* y, int64_t rows, int64_t cols, int64_t ld,
+                  uint32_t axis, void* s) override {
+    Ctx* c = (Ctx*)s;
+    if (!bk.reduce_axis || !bk.axis_ws) return broker::kBadArgument;
+    if (!c->axis_ws && bk.malloc_(&c->axis_ws, bk.axis_ws()) != 0) return broker::kOutOfMemory;
+    return bk.reduce_axis((int)op, (int)dt, x, rows, cols, ld, (int)axis, y, c->axis_ws, c->s);
   }
   const char* last_error() override { return bk.last_error ? bk.last_error() : ""; }
   void info(int64_t v[5]) override {

@@ -9,7 +9,8 @@ const char* op_name(uint32_t op) {
   static const char* const names[] = {"bk.?",        "bk.hello", "bk.alloc",  "bk.free",      "bk.write",
                                       "bk.read",     "bk.rand",  "bk.unary",  "bk.binary",    "bk.cast",
                                       "bk.fill",     "bk.reduce", "bk.gemm",  "bk.transpose", "bk.sync",
-                                      "bk.memstats", "bk.info",  "bk.copy",   "bk.rand_reduce", "bk.alloc_at"};
+                                      "bk.memstats", "bk.info",  "bk.copy",   "bk.rand_reduce", "bk.alloc_at",
+                                      "bk.reduce_axis"};
   return op < sizeof(names) / sizeof(names[0]) ? names[op] : names[0];
 }
 
@@ -345,6 +346,21 @@ int32_t Session::dispatch(uint32_t op, const char* payload, uint64_t len, std::v
         return kBadHandle;
       if (!will_read(bi) || !will_write(bo, 0, ldo == rows ? no : 0)) return kLaunchFailed;
       return dev_.transpose(sdt, ddt, bi->ptr, bo->ptr, rows, cols, ldi, ldo, stream_);
+    }
+    case kReduceAxis: {
+      const uint32_t rop = r.get<uint32_t>(), dt = r.get<uint32_t>();
+      const uint64_t x = r.get<uint64_t>(), y = r.get<uint64_t>();
+      const int64_t rows = r.get<int64_t>(), cols = r.get<int64_t>(), ld = r.get<int64_t>();
+      const uint32_t axis = r.get<uint32_t>();
+      if (!r.ok) return kProtocol;
+      const uint64_t odt_size = dt == 1 ? 8 : 4;
+      uint64_t nx, ny;
+      Buf *bx = lookup(x), *by = lookup(y);
+      if (rop > 1 || axis > 1 || !dtype_size(dt) || dt == 3 || !matrix_bytes(rows, cols, ld, dtype_size(dt), &nx) ||
+          !mul_ok((uint64_t)(axis == 0 ? cols : rows), odt_size, &ny) || !bx || !by || nx > bx->size || ny > by->size)
+        return kBadHandle;
+      if (!will_read(bx) || !will_write(by, 0, ny)) return kLaunchFailed;
+      return dev_.reduce_axis(rop, dt, bx->ptr, by->ptr, rows, cols, ld, axis, stream_);
     }
     case kCopy: {
       const uint64_t d = r.get<uint64_t>(), doff = r.get<uint64_t>(), s = r.get<uint64_t>(), soff = r.get<uint64_t>(),

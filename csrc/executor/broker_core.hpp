@@ -25,7 +25,7 @@ namespace broker {
 
 enum Op : uint32_t {
   kHello = 1, kAlloc, kFree, kWrite, kRead, kRand, kUnary, kBinary, kCast, kFill, kReduce, kGemm, kTranspose,
-  kSync, kMemStats, kInfo, kCopy, kRandReduce, kAllocAt,
+  kSync, kMemStats, kInfo, kCopy, kRandReduce, kAllocAt, kReduceAxis,
   kOpCount
 };
 enum Status : int32_t {
@@ -78,6 +78,9 @@ class Device {
   virtual int gemm(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
                    float beta, int odt, void* s) = 0;
   virtual int transpose(int sdt, int ddt, const void* in, void* out, int rows, int cols, int ldi, int ldo, void* s) = 0;
+  // per-column (axis 0) / per-row (axis 1) sum or mean into y (f64 for f64 x, else f32)
+  virtual int reduce_axis(uint32_t op, uint32_t dt, const void* x, void* y, int64_t rows, int64_t cols, int64_t ld,
+                          uint32_t axis, void* s) = 0;
   virtual const char* last_error() = 0;
   virtual void info(int64_t v[5]) = 0;  // CUs, total, free bytes, clock kHz, LDS/CU
   virtual std::string arch() = 0;

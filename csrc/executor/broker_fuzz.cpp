@@ -121,6 +121,14 @@ class HostDevice final : public Device {
     for (int j = 0; j < cols; ++j) touch_w((char*)out + (uint64_t)j * ldo * so, (uint64_t)rows * so, 0);
     return 0;
   }
+  int reduce_axis(uint32_t op, uint32_t dt, const void* x, void* y, int64_t rows, int64_t cols, int64_t ld,
+                  uint32_t axis, void*) override {
+    if (op > 1 || axis > 1 || dt > 2) return kBadArgument;
+    const uint64_t es = dtype_size(dt), os = dt == 1 ? 8 : 4;
+    for (int64_t r = 0; r < rows; ++r) sum((const char*)x + (uint64_t)r * ld * es, (uint64_t)cols * es);
+    touch_w(y, (uint64_t)(axis == 0 ? cols : rows) * os, 0);
+    return 0;
+  }
   const char* last_error() override { return "host device"; }
   void info(int64_t v[5]) override {
     v[0] = 256;

@@ -206,6 +206,74 @@ int dispatch_reduce(int op, const void* a, const void* b, int64_t n, double* ws,
   return rc;
 }
 
+// ---- axis reductions of a 2-D row-major matrix (numpy sum/mean(axis=)) -------
+// axis 0 (per column): a block of 256 threads owns 256 columns of one row
+// chunk -- each thread walks its column down the chunk, so every wave-row
+// load is 64 consecutive elements; the chunk partials (f64) land in the
+// workspace and a second pass folds them in chunk order (deterministic).
+// axis 1 (per row): one wave per row, lanes stride the row, DPP wave sum.
+constexpr int64_t kAxisWsDoubles = 1 << 18;  // 2 MiB: chunks x columns partials
+
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial(const T* __restrict__ x, int64_t rows, int64_t cols, int64_t ld,
+                                                      int64_t rows_per_chunk, double* __restrict__ part) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= cols) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = r0 + rows_per_chunk < rows ? r0 + rows_per_chunk : rows;
+  double a0 = 0.0, a1 = 0.0;
+  int64_t r = r0;
+  for (; r + 1 < r1; r += 2) {
+    a0 += to_f64<T>(x[r * ld + col]);
+    a1 += to_f64<T>(x[(r + 1) * ld + col]);
+  }
+  if (r < r1) a0 += to_f64<T>(x[r * ld + col]);
+  part[(int64_t)blockIdx.y * cols + col] = a0 + a1;
+}
+
+template <typename TO>
+__global__ __launch_bounds__(256) void colsum_final(const double* __restrict__ part, int chunks, int64_t cols,
+                                                    TO* __restrict__ out, double scale) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= cols) return;
+  double s = 0.0;
+  for (int c = 0; c < chunks; ++c) s += part[(int64_t)c * cols + col];
+  out[col] = (TO)(s * scale);
+}
+
+template <typename T, typename TO>
+__global__ __launch_bounds__(256) void rowsum(const T* __restrict__ x, int64_t rows, int64_t cols, int64_t ld,
+                                              TO* __restrict__ out, double scale) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const T* p = x + row * ld;
+  double acc = 0.0;
+  for (int64_t c = lane; c < cols; c += 64) acc += to_f64<T>(p[c]);
+  acc = wave_reduce<kRedSum>(acc);
+  if (lane == 0) out[row] = (TO)(acc * scale);
+}
+
+template <typename T, typename TO>
+int launch_axis(const T* x, int64_t rows, int64_t cols, int64_t ld, int axis, TO* out, double scale, double* ws,
+                hipStream_t s) {
+  if (axis == 1) {
+    rowsum<T, TO><<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(x, rows, cols, ld, out, scale);
+    return launch_status();
+  }
+  const int64_t col_blocks = (cols + 255) / 256;
+  // enough row chunks to give the chip ~2k blocks, as far as the workspace allows
+  int64_t chunks = 2048 / col_blocks;
+  if (chunks * cols > kAxisWsDoubles) chunks = kAxisWsDoubles / cols;
+  if (chunks > (rows + 31) / 32) chunks = (rows + 31) / 32;
+  if (chunks < 1) chunks = 1;
+  const int64_t per = (rows + chunks - 1) / chunks;
+  chunks = (rows + per - 1) / per;
+  colsum_partial<T><<<dim3((unsigned)col_blocks, (unsigned)chunks), 256, 0, s>>>(x, rows, cols, ld, per, ws);
+  colsum_final<TO><<<(unsigned)col_blocks, 256, 0, s>>>(ws, (int)chunks, cols, out, scale);
+  return launch_status();
+}
+
 }  // namespace bk
 
 using namespace bk;
@@ -248,6 +316,26 @@ BK_API int bk_reduce(int op, int dtype, const void* a, const void* b, int64_t n,
     case kF64: return dispatch_reduce<double>(op, a, b, n, (double*)workspace, (double*)out, stream, Ops{});
     case kF32: return dispatch_reduce<float>(op, a, b, n, (double*)workspace, (double*)out, stream, Ops{});
     case kBF16: return dispatch_reduce<uint16_t>(op, a, b, n, (double*)workspace, (double*)out, stream, Ops{});
+  }
+  return kBadArgument;
+}
+
+BK_API int64_t bk_reduce_axis_workspace_bytes() { return kAxisWsDoubles * (int64_t)sizeof(double); }
+
+// out[cols] (axis 0) or out[rows] (axis 1) = sum (op 0) or mean (op 1) of
+// x[rows x cols] (row stride ld).  out dtype: f64 for f64 input, f32 for f32
+// and bf16 input (f64 accumulation throughout).  ws: the axis workspace.
+BK_API int bk_reduce_axis(int op, int dtype, const void* x, int64_t rows, int64_t cols, int64_t ld, int axis, void* out,
+                          void* ws, hipStream_t stream) {
+  if (!x || !out || !ws || rows <= 0 || cols <= 0 || ld < cols || (axis != 0 && axis != 1) || (op != 0 && op != 1))
+    return kBadArgument;
+  if (axis == 0 && cols > kAxisWsDoubles) return kBadArgument;  // > 262144 columns: reduce a transposed view instead
+  const double scale = op == 1 ? 1.0 / (double)(axis == 0 ? rows : cols) : 1.0;
+  double* w = (double*)ws;
+  switch (dtype) {
+    case kF64: return launch_axis<double, double>((const double*)x, rows, cols, ld, axis, (double*)out, scale, w, stream);
+    case kF32: return launch_axis<float, float>((const float*)x, rows, cols, ld, axis, (float*)out, scale, w, stream);
+    case kBF16: return launch_axis<uint16_t, float>((const uint16_t*)x, rows, cols, ld, axis, (float*)out, scale, w, stream);
   }
   return kBadArgument;
 }

@@ -4,8 +4,8 @@
 # 4096^3 bf16 GEMM of BASELINE config 3.  Same printed lines as the original,
 # plus the GEMM checksum and its independent reference:
 #   sum(A @ B.T) = colsum(A) . colsum(B)
-# (column sums from two ones-row GEMMs, dotted in f64), so every run checks
-# its own GEMM.
+# (column sums by the axis-reduction kernel, dotted in f64), so every run
+# checks its own GEMM.
 import time
 
 import beekern as bk
@@ -23,10 +23,7 @@ def gpu_intensive_computation():
 
 
 def gemm_reference(a, b):
-    ones = bk.ones((256, 4096), dtype="bfloat16")
-    sa = bk.matmul(ones, a, out_dtype="float32")  # every row: the column sums of a
-    sb = bk.matmul(ones, b, out_dtype="float32")
-    return bk.dot(sa.reshape(-1), sb.reshape(-1)) / 256
+    return bk.dot(bk.sum(a, axis=0), bk.sum(b, axis=0))  # column sums, f64-accumulated
 
 
 start_time = time.time()

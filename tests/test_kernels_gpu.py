@@ -463,3 +463,25 @@ def test_bf16_uniform_is_rounded_f32_stream(gpu):
         direct = A.Generator(5).uniform(-1, 1, n, dtype="bfloat16").numpy()
         via_f32 = A.Generator(5).uniform(-1, 1, n, dtype="float32").astype("bfloat16").numpy()
         np.testing.assert_array_equal(direct, via_f32)
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32", "bfloat16"])
+@pytest.mark.parametrize("shape", [(1000, 300), (4096, 4096), (3, 70000), (70000, 3)])
+def test_sum_mean_along_axis(gpu, dtype, shape):
+    """bk.sum / bk.mean(axis=0|1) (bk_reduce_axis: column sums with chunked
+    f64 partials + an ordered fold, row sums one wave per row) against fp64,
+    on plain arrays and on .T views."""
+    rng = np.random.default_rng(sum(shape))
+    h = rng.uniform(-1, 1, shape)
+    if dtype == "bfloat16":
+        h = _bf16_round(h.astype(np.float32)).astype(np.float64)
+    x = gpu.asarray(h, dtype)
+    tol = 1e-9 if dtype == "float64" else 1e-4
+    for axis in (0, 1):
+        got = gpu.sum(x, axis=axis).numpy().astype(np.float64)
+        np.testing.assert_allclose(got, h.sum(axis=axis), rtol=tol, atol=tol * shape[axis])
+        gt = x.T.sum(axis=axis).numpy().astype(np.float64)  # transposed view: the other direction
+        np.testing.assert_allclose(gt, h.T.sum(axis=axis), rtol=tol, atol=tol * shape[1 - axis])
+    np.testing.assert_allclose(gpu.mean(x, axis=0).numpy().astype(np.float64), h.mean(axis=0), rtol=tol, atol=tol)
+    # deterministic: same bits twice
+    assert np.array_equal(gpu.sum(x, axis=0).numpy(), gpu.sum(x, axis=0).numpy())

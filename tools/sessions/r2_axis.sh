@@ -1,0 +1,8 @@
+# Round 2: axis reductions, watchdog, verified payload on MI355X + served-path kernel profile
+source tools/gpu_steps.sh
+export TMPDIR=/tmp
+step gputests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench_default 400 python bench.py
+step bench_np600 300 python bench.py --steps 600
+step prof_served 300 bash tools/prof_served.sh 200
