@@ -23,26 +23,65 @@ import subprocess
 import sys
 from typing import Iterable, List, Set
 
-# import name -> distribution name, for the common mismatches
+# import name -> distribution name where they differ.  The reference resolves
+# imports with upm's pypi_map.sqlite (executor/Dockerfile:30-37,122-124); this
+# table covers the mismatches that code written by LLMs actually hits.
 IMPORT_TO_DIST = {
-    "cv2": "opencv-python",
-    "PIL": "pillow",
-    "sklearn": "scikit-learn",
-    "yaml": "pyyaml",
-    "bs4": "beautifulsoup4",
-    "fitz": "pymupdf",
-    "docx": "python-docx",
-    "pptx": "python-pptx",
-    "dateutil": "python-dateutil",
-    "ffmpeg": "ffmpeg-python",
-    "Crypto": "pycryptodome",
-    "magic": "python-magic",
-    "attr": "attrs",
-    "skimage": "scikit-image",
+    "cv2": "opencv-python-headless", "PIL": "pillow", "sklearn": "scikit-learn", "skimage": "scikit-image",
+    "yaml": "pyyaml", "bs4": "beautifulsoup4", "fitz": "pymupdf", "docx": "python-docx", "pptx": "python-pptx",
+    "dateutil": "python-dateutil", "ffmpeg": "ffmpeg-python", "Crypto": "pycryptodome", "Cryptodome": "pycryptodomex",
+    "magic": "python-magic", "attr": "attrs", "dotenv": "python-dotenv", "jwt": "pyjwt", "serial": "pyserial",
+    "usb": "pyusb", "OpenSSL": "pyopenssl", "git": "gitpython", "github": "pygithub", "telegram": "python-telegram-bot",
+    "discord": "discord.py", "slugify": "python-slugify", "Levenshtein": "python-levenshtein", "pylab": "matplotlib",
+    "mpl_toolkits": "matplotlib", "google": "protobuf", "grpc": "grpcio", "zmq": "pyzmq", "nacl": "pynacl",
+    "jose": "python-jose", "multipart": "python-multipart", "socks": "pysocks", "wx": "wxpython", "gi": "pygobject",
+    "sqlalchemy": "sqlalchemy", "psycopg2": "psycopg2-binary", "MySQLdb": "mysqlclient", "pymysql": "pymysql",
+    "ldap": "python-ldap", "Image": "pillow", "pdfminer": "pdfminer.six",
+    "pdfplumber": "pdfplumber", "PyPDF2": "PyPDF2", "pypdf": "pypdf", "reportlab": "reportlab",
+    "openpyxl": "openpyxl", "xlrd": "xlrd", "xlsxwriter": "xlsxwriter", "odf": "odfpy", "tabulate": "tabulate",
+    "markdown": "markdown", "mistune": "mistune", "lxml": "lxml", "html5lib": "html5lib", "pyquery": "pyquery",
+    "nltk": "nltk", "spacy": "spacy", "gensim": "gensim", "textblob": "textblob", "wordcloud": "wordcloud",
+    "networkx": "networkx", "igraph": "python-igraph", "graphviz": "graphviz", "pydot": "pydot", "shapely": "shapely",
+    "geopandas": "geopandas", "pyproj": "pyproj", "folium": "folium", "plotly": "plotly", "bokeh": "bokeh",
+    "seaborn": "seaborn", "altair": "altair", "statsmodels": "statsmodels", "sympy": "sympy", "xarray": "xarray",
+    "netCDF4": "netcdf4", "h5py": "h5py", "tables": "tables", "pyarrow": "pyarrow", "polars": "polars",
+    "duckdb": "duckdb", "numba": "numba", "llvmlite": "llvmlite", "cython": "cython", "Cython": "cython",
+    "xgboost": "xgboost", "lightgbm": "lightgbm", "catboost": "catboost", "tensorflow": "tensorflow",
+    "keras": "keras", "transformers": "transformers", "tokenizers": "tokenizers", "datasets": "datasets",
+    "sentencepiece": "sentencepiece", "tiktoken": "tiktoken", "imageio": "imageio", "moviepy": "moviepy",
+    "pydub": "pydub", "librosa": "librosa", "soundfile": "soundfile", "sounddevice": "sounddevice",
+    "qrcode": "qrcode", "barcode": "python-barcode", "pyzbar": "pyzbar", "pytesseract": "pytesseract",
+    "pdf2image": "pdf2image", "pikepdf": "pikepdf", "weasyprint": "weasyprint", "pypandoc": "pypandoc",
+    "yt_dlp": "yt-dlp", "youtube_dl": "youtube-dl", "emoji": "emoji", "faker": "faker", "requests": "requests",
+    "httpx": "httpx", "aiohttp": "aiohttp", "websocket": "websocket-client", "websockets": "websockets",
+    "toml": "toml", "tomli": "tomli", "ujson": "ujson", "orjson": "orjson", "simplejson": "simplejson",
+    "jsonschema": "jsonschema", "pydantic": "pydantic", "tqdm": "tqdm", "rich": "rich", "colorama": "colorama",
+    "termcolor": "termcolor", "click": "click", "typer": "typer", "jinja2": "jinja2", "cowsay": "cowsay",
+    "pytz": "pytz", "tzdata": "tzdata", "arrow": "arrow", "pendulum": "pendulum", "babel": "babel",
+    "unidecode": "unidecode", "chardet": "chardet", "cchardet": "cchardet", "regex": "regex",
 }
 
-# provided by the runtime image / stdlib-like names never worth installing
+# distributions the image provides (the reference's requirements.txt:1-4 and
+# requirements-skip.txt:1-24, mapped onto this image) -- never installed ad
+# hoc, so a guess can not shadow the image's build of them
+PREINSTALLED = {
+    # OS-packaged in the reference image
+    "ffmpeg-python", "jinja2", "matplotlib", "moviepy", "numpy", "opencv-python", "opencv-python-headless",
+    "pandas", "pdf2image", "pikepdf", "pillow", "pypandoc", "scipy", "sympy", "tabulate", "xarray", "xonsh",
+    # installed manually there
+    "pymupdf",
+    # requirements.txt
+    "PyPDF2", "pydantic", "pydantic_core",
+    # this image
+    "torch", "beekern", "bee_code_interpreter_fs_amd",
+}
+
+# import names never worth a lookup
 SKIP = {"beekern", "bee_code_interpreter_fs_amd", "__future__", "torch", "numpy", "pandas", "scipy", "matplotlib"}
+
+
+def distribution_for(module: str) -> str:
+    return IMPORT_TO_DIST.get(module, module)
 
 
 def imported_modules(source: str) -> List[str]:
@@ -83,7 +122,9 @@ def install_missing(source: str, target_dir: str, wheelhouse: str = "", timeout:
     missing = missing_modules(imported_modules(source))
     if not missing:
         return []
-    dists = [IMPORT_TO_DIST.get(m, m) for m in missing]
+    dists = [d for d in (distribution_for(m) for m in missing) if d not in PREINSTALLED]
+    if not dists:
+        return []
     cmd = [
         sys.executable, "-m", "pip", "install", "--no-index", "--find-links", wheelhouse,
         "--target", target_dir, "--no-cache-dir", "--quiet", "--disable-pip-version-check", *dists,

@@ -147,3 +147,44 @@ def test_source_file_traceback_names_workspace_path(tmp_path_factory):
         h.stop()
     assert body["exit_code"] == 1
     assert 'File "/workspace/tools/div.py", line 3' in body["stderr"], body["stderr"]
+
+
+# the reference executor image's Python stack (executor/Dockerfile:43-89,
+# requirements.txt): each module gets a tiny real use inside a sandbox; a
+# module this machine does not have is skipped, not failed (the deploy image,
+# deploy/Dockerfile + deploy/requirements-sandbox.txt, installs them all)
+STACK = {
+    "sympy": "import sympy\nx = sympy.symbols('x')\nprint(sympy.integrate(x**2, (x, 0, 3)))",
+    "tabulate": "from tabulate import tabulate\nprint(tabulate([[1, 2]], headers=['a', 'b'], tablefmt='plain').split()[0])",
+    "jinja2": "import jinja2\nprint(jinja2.Template('{{ a }}+{{ b }}').render(a=1, b=2))",
+    "xarray": "import xarray as xr, numpy as np\nprint(float(xr.DataArray(np.arange(4.0)).sum()))",
+    "cv2": "import cv2, numpy as np\nprint(cv2.cvtColor(np.zeros((2, 2, 3), np.uint8), cv2.COLOR_BGR2GRAY).shape)",
+    "pikepdf": "import pikepdf\npdf = pikepdf.new(); pdf.add_blank_page(); print(len(pdf.pages))",
+    "fitz": "import fitz\nprint(len(fitz.open()))",
+    "PyPDF2": "import PyPDF2\nprint(PyPDF2.__version__.split('.')[0])",
+    "moviepy": "import moviepy\nprint('moviepy ok')",
+    "pdf2image": "import pdf2image\nprint('pdf2image ok')",
+    "openpyxl": "import openpyxl\nwb = openpyxl.Workbook(); print(wb.active.title)",
+}
+EXPECT = {"sympy": "9", "tabulate": "a", "jinja2": "1+2", "xarray": "6.0", "cv2": "(2, 2)", "pikepdf": "1",
+          "fitz": "0", "PyPDF2": "2", "moviepy": "moviepy ok", "pdf2image": "pdf2image ok", "openpyxl": "Sheet"}
+
+
+@pytest.mark.parametrize("module", sorted(STACK))
+def test_reference_image_stack(stub, module):
+    pytest.importorskip(module)
+    r = stub.Execute(pb.ExecuteRequest(source_code=STACK[module]), timeout=120)
+    assert r.exit_code == 0, r.stderr
+    assert r.stdout.strip() == EXPECT[module], r.stdout
+
+
+def test_import_to_distribution_and_preinstalled():
+    from bee_code_interpreter_fs_amd.runtime import deps
+
+    assert deps.distribution_for("cv2") == "opencv-python-headless"
+    assert deps.distribution_for("fitz") == "pymupdf" and deps.distribution_for("yt_dlp") == "yt-dlp"
+    assert deps.distribution_for("somethingelse") == "somethingelse"
+    # the image's own stack is never re-installed ad hoc (requirements-skip.txt)
+    for name in ("ffmpeg-python", "pymupdf", "opencv-python-headless", "PyPDF2", "sympy"):
+        assert name in deps.PREINSTALLED
+    assert deps.imported_modules("import cv2, os\nfrom fitz import open as o\nimport yt_dlp.utils") == ["cv2", "os", "fitz", "yt_dlp"]
