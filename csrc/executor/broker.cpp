@@ -94,7 +94,25 @@ class HipDevice final : public broker::Device {
     void* scalar = nullptr;  // device fallback when no pinned slot exists
     double* slot = nullptr;
     void* axis_ws = nullptr;  // axis-reduction partials, allocated on first use
+    // frees waiting for the stream work recorded before them (event, buffer)
+    std::vector<std::pair<hipEvent_t, void*>> pending;
+    std::vector<hipEvent_t> spare_events;
   };
+
+  // free the buffers whose recorded stream work has completed
+  void reap(Ctx* c, bool all) {
+    size_t keep = 0;
+    for (size_t i = 0; i < c->pending.size(); ++i) {
+      auto& pe = c->pending[i];
+      if (all || hipEventQuery(pe.first) == hipSuccess) {
+        bk.free_(pe.second);
+        c->spare_events.push_back(pe.first);
+      } else {
+        c->pending[keep++] = pe;
+      }
+    }
+    c->pending.resize(keep);
+  }
 
   bool load(const std::string& path, std::string* err) {
     lib_ = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
@@ -172,8 +190,32 @@ class HipDevice final : public broker::Device {
     return c;
   }
   void give_stream(void* p) override {
+    Ctx* c = (Ctx*)p;
+    reap(c, true);  // the session drained the stream before handing it back
     std::lock_guard<std::mutex> lk(mu_);
-    pool_.push_back((Ctx*)p);
+    pool_.push_back(c);
+  }
+  void release(void* p, void* s) override {
+    // a free used to be a stream sync: the session blocked until the GPU
+    // caught up.  Now the buffer waits on an event instead.
+    Ctx* c = (Ctx*)s;
+    reap(c, false);
+    hipEvent_t ev = nullptr;
+    if (!c->spare_events.empty()) {
+      ev = c->spare_events.back();
+      c->spare_events.pop_back();
+    } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      hipStreamSynchronize(c->s);
+      bk.free_(p);
+      return;
+    }
+    if (hipEventRecord(ev, c->s) != hipSuccess) {
+      c->spare_events.push_back(ev);
+      hipStreamSynchronize(c->s);
+      bk.free_(p);
+      return;
+    }
+    c->pending.emplace_back(ev, p);
   }
   static hipStream_t st(void* p) { return ((Ctx*)p)->s; }
 

@@ -184,9 +184,8 @@ int32_t Session::dispatch(uint32_t op, const char* payload, uint64_t len, std::v
       const uint64_t h = r.get<uint64_t>();
       auto it = bufs_.find(h);
       if (!r.ok || it == bufs_.end()) return kBadHandle;
-      dev_.sync(stream_);  // no queued kernel may still use it
       const uint64_t rounded = charged_bytes(it->second.size);
-      dev_.free(it->second.ptr);
+      dev_.release(it->second.ptr, stream_);  // back to the allocator once queued work is done with it
       conn_bytes_ -= (int64_t)rounded;
       peer_.account->refund((int64_t)rounded);
       if (live_) *live_ -= (int64_t)rounded;

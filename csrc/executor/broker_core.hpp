@@ -59,6 +59,13 @@ class Device {
   virtual void give_stream(void* s) = 0;  // drained
   virtual int malloc(void** p, uint64_t nbytes) = 0;
   virtual void free(void* p) = 0;
+  // a buffer the session is done with while work queued on `s` may still use
+  // it: returned to the allocator once that work has finished (by default
+  // after a stream sync; the HIP device defers it with an event instead)
+  virtual void release(void* p, void* s) {
+    sync(s);
+    free(p);
+  }
   virtual bool zero_async(void* p, uint64_t nbytes, void* s) = 0;
   virtual bool h2d_sync(void* dst, const void* src, uint64_t n, void* s) = 0;
   virtual bool d2h_sync(void* dst, const void* src, uint64_t n, void* s) = 0;

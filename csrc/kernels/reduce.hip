@@ -231,14 +231,50 @@ __global__ __launch_bounds__(256) void colsum_partial(const T* __restrict__ x, i
   part[(int64_t)blockIdx.y * cols + col] = a0 + a1;
 }
 
+// 16-B vectors per lane (V columns), 4 row groups per block: a wave reads one
+// contiguous 1 KiB (bf16) row segment per step
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial_v(const T* __restrict__ x, int64_t rows, int64_t cols, int64_t ld,
+                                                        int64_t rows_per_chunk, double* __restrict__ part) {
+  constexpr int V = 16 / sizeof(T);
+  __shared__ double sacc[4][64 * V];
+  const int tx = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t col0 = ((int64_t)blockIdx.x * 64 + tx) * V;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = r0 + rows_per_chunk < rows ? r0 + rows_per_chunk : rows;
+  double acc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) acc[j] = 0.0;
+  if (col0 < cols) {
+    for (int64_t r = r0 + g; r < r1; r += 4) {
+      const V16<T> v = *reinterpret_cast<const V16<T>*>(x + r * ld + col0);
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[j] += to_f64<T>(v.v[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) sacc[g][tx * V + j] = acc[j];
+  __syncthreads();
+  // 256 threads fold the 4 row groups of 64*V columns
+  for (int c = threadIdx.x; c < 64 * V; c += 256) {
+    const int64_t col = (int64_t)blockIdx.x * 64 * V + c;
+    if (col < cols) part[(int64_t)blockIdx.y * cols + col] = sacc[0][c] + sacc[1][c] + sacc[2][c] + sacc[3][c];
+  }
+}
+
+// fold the chunk partials: 4 threads per column (strided chunks), LDS combine
 template <typename TO>
 __global__ __launch_bounds__(256) void colsum_final(const double* __restrict__ part, int chunks, int64_t cols,
                                                     TO* __restrict__ out, double scale) {
-  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (col >= cols) return;
+  __shared__ double s4[4][64];
+  const int tx = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
   double s = 0.0;
-  for (int c = 0; c < chunks; ++c) s += part[(int64_t)c * cols + col];
-  out[col] = (TO)(s * scale);
+  if (col < cols)
+    for (int c = g; c < chunks; c += 4) s += part[(int64_t)c * cols + col];
+  s4[g][tx] = s;
+  __syncthreads();
+  if (g == 0 && col < cols) out[col] = (TO)(((s4[0][tx] + s4[1][tx]) + (s4[2][tx] + s4[3][tx])) * scale);
 }
 
 template <typename T, typename TO>
@@ -261,16 +297,22 @@ int launch_axis(const T* x, int64_t rows, int64_t cols, int64_t ld, int axis, TO
     rowsum<T, TO><<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(x, rows, cols, ld, out, scale);
     return launch_status();
   }
-  const int64_t col_blocks = (cols + 255) / 256;
-  // enough row chunks to give the chip ~2k blocks, as far as the workspace allows
-  int64_t chunks = 2048 / col_blocks;
+  constexpr int V = 16 / sizeof(T);
+  const bool vec = cols % V == 0 && ld % V == 0 && ((uintptr_t)x & 15) == 0;
+  const int64_t col_blocks = vec ? (cols + 64 * V - 1) / (64 * V) : (cols + 255) / 256;
+  // enough row chunks for ~1k blocks, as far as the workspace allows; each
+  // chunk at least 32 rows so a lane streams several vectors
+  int64_t chunks = 1024 / col_blocks;
   if (chunks * cols > kAxisWsDoubles) chunks = kAxisWsDoubles / cols;
   if (chunks > (rows + 31) / 32) chunks = (rows + 31) / 32;
   if (chunks < 1) chunks = 1;
   const int64_t per = (rows + chunks - 1) / chunks;
   chunks = (rows + per - 1) / per;
-  colsum_partial<T><<<dim3((unsigned)col_blocks, (unsigned)chunks), 256, 0, s>>>(x, rows, cols, ld, per, ws);
-  colsum_final<TO><<<(unsigned)col_blocks, 256, 0, s>>>(ws, (int)chunks, cols, out, scale);
+  if (vec)
+    colsum_partial_v<T><<<dim3((unsigned)col_blocks, (unsigned)chunks), 256, 0, s>>>(x, rows, cols, ld, per, ws);
+  else
+    colsum_partial<T><<<dim3((unsigned)col_blocks, (unsigned)chunks), 256, 0, s>>>(x, rows, cols, ld, per, ws);
+  colsum_final<TO><<<(unsigned)((cols + 63) / 64), 256, 0, s>>>(ws, (int)chunks, cols, out, scale);
   return launch_status();
 }
 
