@@ -194,6 +194,12 @@ class BrokerDriver:
         self._next = 1  # client handle ids (the broker's own start at 2**62)
         self._sizes: dict = {}
         self._charged = 0
+        # fire-and-forget frames waiting to go out with the next request that
+        # wants a reply (or a flush): one send and one broker wake-up per
+        # batch instead of per launch
+        self._out = bytearray()
+        self._out_frames = 0
+        self._rbuf = bytearray(4096)
 
     def init(self, device: int, lazy: bool = False) -> None:
         """Open the broker session (connect + HELLO); with ``lazy`` the
@@ -207,6 +213,9 @@ class BrokerDriver:
         s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
         s.connect(self.path)
         self.sock = s
+        import atexit
+
+        atexit.register(self.flush)  # queued launches still reach the GPU at exit
         payload = self._call(HELLO, b"")
         (self.quota,) = struct.unpack_from("<q", payload, 0)
         (n,) = struct.unpack_from("<I", payload, 8)
@@ -225,20 +234,39 @@ class BrokerDriver:
             self._connect()
         hdr = _HDR.pack(op, 0, len(payload))
         with self.lock:
-            if len(payload) < (1 << 16):
+            if self._out:
+                # queued launches go first, in the same send
+                self._out += hdr
+                self._out += payload
+                frame, self._out, self._out_frames = self._out, bytearray(), 0
+                self.sock.sendall(frame)
+            elif len(payload) < (1 << 16):
                 self.sock.sendall(hdr + payload)
             else:
                 self.sock.sendall(hdr)
                 self.sock.sendall(payload)
-            hdr = bytearray(_RHDR.size)
-            self._recv_into(memoryview(hdr))
-            status, _, n = _RHDR.unpack(hdr)
+            # the broker sends header and body in one message: one recv
+            # usually takes both
+            view = memoryview(self._rbuf)
+            got = 0
+            while got < _RHDR.size:
+                k = self.sock.recv_into(view[got:])
+                if k == 0:
+                    raise BeekernError("kernel broker closed the connection")
+                got += k
+            status, _, n = _RHDR.unpack_from(self._rbuf, 0)
+            have = got - _RHDR.size
+            if have > n:
+                raise BeekernError("kernel broker: protocol error (reply longer than announced)")
             if status == 0 and out is not None and n == len(out):
-                self._recv_into(out)
+                out[:have] = view[_RHDR.size : got]
+                if n > have:
+                    self._recv_into(out[have:])
                 return b""
             body = bytearray(n)
-            if n:
-                self._recv_into(memoryview(body))
+            body[:have] = view[_RHDR.size : got]
+            if n > have:
+                self._recv_into(memoryview(body)[have:])
         if status != 0:
             msg = {1: "bad argument", 2: "launch failed", 3: "out of device memory", 4: "HBM quota exceeded",
                    5: "not initialised", 6: "bad handle / out of bounds", 7: "protocol error"}.get(status, str(status))
@@ -254,11 +282,32 @@ class BrokerDriver:
     def _post(self, op: int, payload: bytes) -> None:
         """Fire-and-forget request (kernel launches, frees): no reply; a
         failure is raised by the next request that waits for one (sync,
-        reduce, read, alloc) -- the asynchronous-error model of GPU streams."""
+        reduce, read, alloc) -- the asynchronous-error model of GPU streams.
+        Frames are queued and leave with that next request (or once the
+        queue holds 64 frames / 64 KB, on flush(), or at exit)."""
         if self.sock is None:
             self._connect()
         with self.lock:
-            self.sock.sendall(_HDR.pack(op, _NO_REPLY, len(payload)) + payload)
+            self._out += _HDR.pack(op, _NO_REPLY, len(payload))
+            self._out += payload
+            self._out_frames += 1
+            if self._out_frames >= 64 or len(self._out) >= (64 << 10):
+                self._flush_locked()
+
+    def _flush_locked(self) -> None:
+        if self._out:
+            frame, self._out, self._out_frames = self._out, bytearray(), 0
+            self.sock.sendall(frame)
+
+    def flush(self) -> None:
+        """Send queued launches now (without waiting for them)."""
+        if self.sock is None:
+            return
+        with self.lock:
+            try:
+                self._flush_locked()
+            except OSError:
+                pass
 
     def malloc(self, nbytes: int) -> int:
         nbytes = max(int(nbytes), 1)

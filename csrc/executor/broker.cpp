@@ -17,30 +17,6 @@ namespace bee {
 
 namespace {
 
-bool read_exact(int fd, void* buf, size_t n) {
-  char* p = (char*)buf;
-  while (n > 0) {
-    ssize_t r = recv(fd, p, n, 0);
-    if (r < 0 && errno == EINTR) continue;
-    if (r <= 0) return false;
-    p += r;
-    n -= (size_t)r;
-  }
-  return true;
-}
-
-bool send_exact(int fd, const void* buf, size_t n) {
-  const char* p = (const char*)buf;
-  while (n > 0) {
-    ssize_t w = send(fd, p, n, MSG_NOSIGNAL);
-    if (w < 0 && errno == EINTR) continue;
-    if (w <= 0) return false;
-    p += w;
-    n -= (size_t)w;
-  }
-  return true;
-}
-
 // roctx range per op: `rocprofv3 --marker-trace --kernel-trace` of the
 // daemon shows which sandbox request each broker kernel belongs to (a table
 // lookup when no profiler is attached)
@@ -415,26 +391,18 @@ void KernelBroker::serve(int fd, pid_t peer_pid) {
   {
     broker::Session session(*dev_, std::move(peer), &live_bytes_);
     std::vector<char> payload, reply;
+    broker::FrameReader frames(fd);
     while (!stopping_) {
       uint32_t hdr[4];
-      if (!read_exact(fd, hdr, sizeof hdr)) break;
-      uint64_t len;
-      memcpy(&len, &hdr[2], 8);
-      if (len > broker::kMaxFrame) break;
-      payload.resize(len);
-      if (len && !read_exact(fd, payload.data(), len)) break;
+      if (!frames.next(hdr, &payload)) break;
+      const uint64_t len = payload.size();
       CpuScope cpu(kCpuBroker);
       RoctxRange range(broker::op_name(hdr[0]));
       ops_++;
       bool send = false;
       const int32_t st = session.handle(hdr[0], hdr[1], payload.data(), len, &reply, &send);
       if (!send) continue;
-      uint32_t rh[4];
-      memcpy(&rh[0], &st, 4);
-      rh[1] = 0;
-      const uint64_t olen = reply.size();
-      memcpy(&rh[2], &olen, 8);
-      if (!send_exact(fd, rh, sizeof rh) || (olen && !send_exact(fd, reply.data(), olen))) break;
+      if (!broker::send_reply(fd, st, &reply)) break;
     }
   }  // session end: drain, free, refund
   close(fd);

@@ -1,5 +1,10 @@
 #include "broker_core.hpp"
 
+#include <errno.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <cstring>
 
 namespace bee {
@@ -389,6 +394,89 @@ int32_t Session::dispatch(uint32_t op, const char* payload, uint64_t len, std::v
     }
   }
   return kProtocol;
+}
+
+namespace {
+
+bool read_full(int fd, char* p, size_t n) {
+  while (n) {
+    const ssize_t r = read(fd, p, n);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    p += r;
+    n -= (size_t)r;
+  }
+  return true;
+}
+
+bool write_full(int fd, const char* p, size_t n) {
+  while (n) {
+    const ssize_t w = send(fd, p, n, MSG_NOSIGNAL);
+    if (w < 0 && errno == EINTR) continue;
+    if (w < 0 && errno == ENOTSOCK) {  // a pipe (the fuzz harness)
+      const ssize_t v = write(fd, p, n);
+      if (v <= 0) return false;
+      p += v;
+      n -= (size_t)v;
+      continue;
+    }
+    if (w <= 0) return false;
+    p += w;
+    n -= (size_t)w;
+  }
+  return true;
+}
+
+}  // namespace
+
+std::atomic<uint64_t> FrameReader::reads_{0};
+
+bool FrameReader::take(void* dst, size_t n) {
+  char* d = (char*)dst;
+  const size_t k = std::min(end_ - beg_, n);
+  memcpy(d, buf_.data() + beg_, k);
+  beg_ += k;
+  d += k;
+  n -= k;
+  if (!n) return true;
+  beg_ = end_ = 0;
+  if (n >= buf_.size()) return read_full(fd_, d, n);  // bulk payload: straight in
+  while (end_ < n) {
+    reads_.fetch_add(1, std::memory_order_relaxed);
+    const ssize_t r = read(fd_, buf_.data() + end_, buf_.size() - end_);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    end_ += (size_t)r;
+  }
+  memcpy(d, buf_.data(), n);
+  beg_ = n;
+  return true;
+}
+
+bool FrameReader::next(uint32_t hdr[4], std::vector<char>* payload, bool* too_large) {
+  if (too_large) *too_large = false;
+  if (!take(hdr, 16)) return false;
+  uint64_t len;
+  memcpy(&len, &hdr[2], 8);
+  if (len > max_) {
+    if (too_large) *too_large = true;
+    return false;
+  }
+  payload->resize(len);
+  return !len || take(payload->data(), len);
+}
+
+bool send_reply(int fd, int32_t status, std::vector<char>* reply) {
+  uint32_t rh[4];
+  memcpy(&rh[0], &status, 4);
+  rh[1] = 0;
+  const uint64_t olen = reply->size();
+  memcpy(&rh[2], &olen, 8);
+  if (olen <= (64u << 10)) {
+    reply->insert(reply->begin(), (const char*)rh, (const char*)rh + sizeof rh);
+    return write_full(fd, reply->data(), reply->size());
+  }
+  return write_full(fd, (const char*)rh, sizeof rh) && write_full(fd, reply->data(), olen);
 }
 
 }  // namespace broker

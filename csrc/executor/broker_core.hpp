@@ -114,6 +114,30 @@ struct Peer {
   std::shared_ptr<Account> account;
 };
 
+// Frames of one connection, read through a 64 KB buffer: a client that
+// queues its fire-and-forget launches (ops/driver.py BrokerDriver._post)
+// delivers a batch in one send, and this takes it in one read
+class FrameReader {
+ public:
+  explicit FrameReader(int fd, uint64_t max_frame = kMaxFrame) : fd_(fd), max_(max_frame), buf_(64 << 10) {}
+  // the next frame's header and payload; false on EOF, error or a frame
+  // longer than max_frame (*too_large set)
+  bool next(uint32_t hdr[4], std::vector<char>* payload, bool* too_large = nullptr);
+  static uint64_t reads() { return reads_.load(std::memory_order_relaxed); }  // read() calls, all readers
+
+ private:
+  static std::atomic<uint64_t> reads_;
+  bool take(void* dst, size_t n);
+  int fd_;
+  uint64_t max_;
+  std::vector<char> buf_;
+  size_t beg_ = 0, end_ = 0;
+};
+
+// response header and payload in one write when it is small (one read takes
+// both on the client); *reply is consumed
+bool send_reply(int fd, int32_t status, std::vector<char>* reply);
+
 class Session {
  public:
   Session(Device& dev, Peer peer, std::atomic<int64_t>* live_bytes);

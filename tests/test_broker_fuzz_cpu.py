@@ -219,3 +219,81 @@ def _random_frames(seed: int, n: int):
 def test_random_frames_no_sanitizer_findings(fuzz_bin, seed):
     rows = run(fuzz_bin, _random_frames(seed, 3000), budget=32 << 20, quota=24 << 20)
     assert len(rows) > 3000
+
+
+# ---- the Python client against the daemon's frame I/O -------------------------------
+
+
+def _serve(fuzz_bin, path, budget=64 << 20, quota=0):
+    p = subprocess.Popen([fuzz_bin, "--listen", path, str(budget), str(quota)], stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE,
+                         env={**os.environ, "ASAN_OPTIONS": "abort_on_error=1:detect_leaks=1",
+                              "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"})
+    assert p.stdout.readline().strip() == b"LISTENING"
+    return p
+
+
+def _finish(p):
+    out, err = p.communicate(timeout=60)
+    err = err.decode(errors="replace")
+    assert p.returncode == 0 and "AddressSanitizer" not in err and "runtime error" not in err, err[-4000:]
+    line = out.decode().strip().splitlines()[-1]
+    assert line.startswith("SERVED"), line
+    return dict(kv.split("=") for kv in line.split()[1:])
+
+
+def test_client_batches_launches_into_one_send(fuzz_bin, tmp_path):
+    """BrokerDriver queues fire-and-forget frames and sends them with the
+    next request that wants a reply: the daemon's reader takes a batch in
+    one read, replies (header + body) arrive in one message, and the
+    deferred-error model still holds."""
+    import numpy as np
+
+    from bee_code_interpreter_fs_amd.ops.driver import BeekernError, BrokerDriver
+
+    path = str(tmp_path / "b.sock")
+    p = _serve(fuzz_bin, path)
+    d = BrokerDriver(path)
+    d.init(0)
+    hs = [d.malloc(4096) for _ in range(8)]     # 8 queued ALLOC_AT
+    for h in hs:
+        d.fill(h, 4096, 0x0101010101010101, 8)  # 8 queued FILL
+    host = np.zeros(4096, dtype=np.uint8)
+    d.d2h(hs[3], host)                            # the batch goes out with this READ
+    assert (host == 1).all()
+    big = np.arange(1 << 20, dtype=np.uint8)      # > one read buffer: straight-in path both ways
+    hb = d.malloc(big.nbytes)
+    d.h2d(hb, big)
+    back = np.empty_like(big)
+    d.d2h(hb, back)
+    assert (back == big).all()
+    d.copy(hs[0], 12345 << 20, 16)                # bad handle, queued: reported by the next reply
+    with pytest.raises(BeekernError, match="bad handle"):
+        d.sync()
+    d.free(hs[1])
+    d.flush()
+    d.sock.close()
+    stats = _finish(p)
+    assert int(stats["frames"]) == 1 + 8 + 8 + 1 + 1 + 1 + 1 + 1 + 1 + 1
+    assert int(stats["replies"]) == 5            # HELLO, 2x READ, WRITE, SYNC
+    # HELLO, the 17-frame batch, 1 MiB WRITE (chunked reads), READ, copy+sync, free: far fewer reads than frames
+    assert int(stats["reads"]) < int(stats["frames"])
+    assert stats["live"] == "0"
+
+
+def test_client_queue_flushes_at_64_frames(fuzz_bin, tmp_path):
+    from bee_code_interpreter_fs_amd.ops.driver import BrokerDriver
+
+    path = str(tmp_path / "b.sock")
+    p = _serve(fuzz_bin, path)
+    d = BrokerDriver(path)
+    d.init(0)
+    h = d.malloc(1 << 12)
+    for _ in range(200):
+        d.fill(h, 1 << 12, 7, 8)
+    assert d._out_frames == (200 + 1) % 64      # the rest left in full batches
+    d.sync()
+    assert d._out_frames == 0 and not d._out
+    d.sock.close()
+    stats = _finish(p)
+    assert int(stats["frames"]) == 1 + 1 + 200 + 1
