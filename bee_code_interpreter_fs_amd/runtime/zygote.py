@@ -152,10 +152,27 @@ def _native_loop():
     return _zygote_loop
 
 
+def _thp_module():
+    """The huge-page heap helpers of ``_zygote_loop`` (see
+    csrc/zygote/zygote_loop.cpp), unless ``BEE_ZYGOTE_THP=0`` or not built."""
+    if os.environ.get("BEE_ZYGOTE_THP", "1") == "0":
+        return None
+    try:
+        from . import _zygote_loop
+    except ImportError:
+        return None
+    return _zygote_loop
+
+
 def main() -> None:
     fd = int(os.environ["BEE_ZYGOTE_FD"])
     chan = socket.socket(fileno=fd)
     t0 = time.perf_counter()
+    # fork + exit cost scales with the zygote's page tables: put the heap the
+    # preload is about to build on 2 MB pages (pymalloc arenas now, the rest
+    # collapsed once the preload is done)
+    thp = _thp_module()
+    thp_on = bool(thp is not None and thp.thp_arenas())
     loaded = _preload()
     import_ms = (time.perf_counter() - t0) * 1e3
     if _hip_initialized():
@@ -166,6 +183,9 @@ def main() -> None:
     if n_rules is not None:
         loaded.append(f"jail:{n_rules}-rules")
     _freeze_for_fork()
+    if thp_on:
+        collapsed, _ = thp.thp_collapse()
+        loaded.append(f"thp:{collapsed >> 20}MB")
     try:
         libc = ctypes.CDLL(None)
         libc.prctl(PR_SET_CHILD_SUBREAPER, 1, 0, 0, 0)
@@ -296,6 +316,8 @@ def main() -> None:
                         continue
                     if pid == 0:
                         # ---- child ----
+                        if thp_on:
+                            thp.thp_child()
                         if debug:
                             worker._cpu_stamp_force("child_entry")
                         # drop the zygote's signal plumbing and descriptors

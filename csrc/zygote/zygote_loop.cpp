@@ -26,6 +26,7 @@
 #include <signal.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/signalfd.h>
 #include <sys/wait.h>
 #include <time.h>
@@ -35,6 +36,139 @@
 #include <unordered_set>
 
 namespace {
+
+// ---- huge-page backed heap ------------------------------------------------
+//
+// Every sandbox costs the zygote a fork() and the sandbox an exit(); both
+// walk the page tables of the zygote's private memory (copy them, tear them
+// down) -- ~30 us per MB each, measured: at 4 KB pages the preloaded Python
+// heap alone made fork+exit the largest per-request CPU item after the
+// sandbox's own Python.  Mapped with 2 MB pages (transparent huge pages) the
+// same memory is one page-table entry per 2 MB: 256 MB forks+exits in
+// ~0.4 ms instead of ~13 ms.  A child's first write to a shared huge page
+// still copies only 4 KB (the kernel splits the mapping in the child).
+//
+// pymalloc's 1 MiB arenas are carved from one MADV_HUGEPAGE region
+// (thp_arenas), and the rest of the zygote's anonymous memory -- glibc's
+// heap, numpy's buffers -- is collapsed into huge pages once preloading is
+// done (thp_collapse).  Children switch the region back to small pages
+// (their new arenas should not fault in 2 MB at a time).
+
+constexpr size_t kHuge = 2u << 20;
+#ifndef MADV_COLLAPSE
+#define MADV_COLLAPSE 25
+#endif
+
+struct ArenaRegion {
+  char* base = nullptr;
+  size_t size = 0, used = 0;
+  void* freed[1024];
+  size_t nfreed = 0;
+  size_t arenas = 0, fallbacks = 0;
+  PyObjectArenaAllocator prev{};
+} g_arena;
+
+void* arena_alloc(void*, size_t n) {
+  ArenaRegion& r = g_arena;
+  for (size_t i = 0; i < r.nfreed; ++i)  // arenas are all one size; keep it simple
+    if (r.freed[i]) {
+      void* p = r.freed[i];
+      r.freed[i] = r.freed[--r.nfreed];
+      r.arenas++;
+      return p;
+    }
+  if (r.base && n <= r.size - r.used) {
+    void* p = r.base + r.used;
+    r.used += n;
+    r.arenas++;
+    return p;
+  }
+  r.fallbacks++;
+  void* p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  return p == MAP_FAILED ? nullptr : p;
+}
+
+void arena_free(void*, void* p, size_t n) {
+  ArenaRegion& r = g_arena;
+  if (r.base && (char*)p >= r.base && (char*)p < r.base + r.size) {
+    if (r.nfreed < sizeof r.freed / sizeof r.freed[0]) r.freed[r.nfreed++] = p;
+    return;  // (a full free list leaks the arena's address range, not memory the zygote uses)
+  }
+  munmap(p, n);  // arenas from before the switch, or fallbacks: plain mmaps
+}
+
+PyObject* thp_arenas(PyObject*, PyObject* args) {
+  unsigned long long reserve = 1ull << 30;
+  if (!PyArg_ParseTuple(args, "|K", &reserve)) return nullptr;
+  if (g_arena.base) Py_RETURN_TRUE;
+  reserve = (reserve + kHuge - 1) & ~(unsigned long long)(kHuge - 1);
+  // over-map by one huge page and trim to 2 MB alignment
+  char* raw = (char*)mmap(nullptr, reserve + kHuge, PROT_READ | PROT_WRITE,
+                          MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  if (raw == MAP_FAILED) Py_RETURN_FALSE;
+  char* base = (char*)(((uintptr_t)raw + kHuge - 1) & ~(uintptr_t)(kHuge - 1));
+  if (base > raw) munmap(raw, (size_t)(base - raw));
+  const size_t tail = (size_t)(raw + reserve + kHuge - (base + reserve));
+  if (tail) munmap(base + reserve, tail);
+  if (madvise(base, reserve, MADV_HUGEPAGE) != 0) {
+    munmap(base, reserve);
+    Py_RETURN_FALSE;  // THP unavailable ("never"): leave pymalloc alone
+  }
+  g_arena.base = base;
+  g_arena.size = reserve;
+  PyObject_GetArenaAllocator(&g_arena.prev);
+  PyObjectArenaAllocator a{nullptr, arena_alloc, arena_free};
+  PyObject_SetArenaAllocator(&a);
+  Py_RETURN_TRUE;
+}
+
+// MADV_COLLAPSE every 2 MB-aligned, populated stretch of the process's
+// private anonymous memory (heap and anonymous mappings); returns
+// (collapsed_bytes, tried_bytes)
+PyObject* thp_collapse(PyObject*, PyObject*) {
+  FILE* f = fopen("/proc/self/maps", "re");
+  if (!f) return PyErr_SetFromErrno(PyExc_OSError);
+  struct Range {
+    uintptr_t a, b;
+  };
+  std::string ranges;  // packed Range records (no allocation while parsing)
+  char line[512];
+  while (fgets(line, sizeof line, f)) {
+    unsigned long a, b, off;
+    char perms[8] = {0}, dev[16] = {0};
+    unsigned long inode;
+    int name_at = 0;
+    if (sscanf(line, "%lx-%lx %7s %lx %15s %lu %n", &a, &b, perms, &off, dev, &inode, &name_at) < 6) continue;
+    const char* name = line + name_at;
+    const bool anon = inode == 0 && (name[0] == '\n' || name[0] == 0 || strncmp(name, "[heap]", 6) == 0);
+    if (!anon || perms[0] != 'r' || perms[1] != 'w' || perms[3] != 'p') continue;
+    Range r{(a + kHuge - 1) & ~(uintptr_t)(kHuge - 1), b & ~(uintptr_t)(kHuge - 1)};
+    if (r.b > r.a) ranges.append((const char*)&r, sizeof r);
+  }
+  fclose(f);
+  unsigned long long ok = 0, tried = 0;
+  for (size_t i = 0; i + sizeof(Range) <= ranges.size(); i += sizeof(Range)) {
+    Range r;
+    memcpy(&r, ranges.data() + i, sizeof r);
+    for (uintptr_t p = r.a; p < r.b; p += kHuge) {
+      tried += kHuge;
+      if (madvise((void*)p, kHuge, MADV_COLLAPSE) == 0) ok += kHuge;  // EINVAL/EAGAIN: empty or busy
+    }
+  }
+  return Py_BuildValue("(KK)", ok, tried);
+}
+
+PyObject* thp_stats(PyObject*, PyObject*) {
+  return Py_BuildValue("{s:K,s:K,s:K,s:K}", "reserved", (unsigned long long)g_arena.size, "used",
+                       (unsigned long long)g_arena.used, "arenas", (unsigned long long)g_arena.arenas, "fallbacks",
+                       (unsigned long long)g_arena.fallbacks);
+}
+
+// in a forked child: new arenas on 4 KB pages (a sandbox's own allocations
+// should not fault in 2 MB at a time); the inherited huge pages stay
+void thp_child() {
+  if (g_arena.base) madvise(g_arena.base, g_arena.size, MADV_NOHUGEPAGE);
+}
 
 double mono_s() {
   timespec ts;
@@ -250,6 +384,7 @@ PyObject* serve(PyObject*, PyObject* args) {
           signal(SIGCHLD, SIG_DFL);
           signal(SIGTERM, SIG_DFL);
           sigprocmask(SIG_SETMASK, &old, nullptr);
+          thp_child();
           return PyBytes_FromStringAndSize(line.data(), (Py_ssize_t)line.size());
         }
         children.insert(pid);
@@ -270,6 +405,13 @@ PyMethodDef kMethods[] = {
     {"serve", serve, METH_VARARGS,
      "serve(chan_fd) -> bytes | None: run the zygote loop; returns the spawn line in a forked child, None when "
      "the executor closes the channel or SIGTERM arrives."},
+    {"thp_arenas", thp_arenas, METH_VARARGS,
+     "thp_arenas(reserve_bytes=1 GiB) -> bool: carve pymalloc arenas from a huge-page region from now on."},
+    {"thp_collapse", thp_collapse, METH_NOARGS,
+     "thp_collapse() -> (collapsed_bytes, tried_bytes): MADV_COLLAPSE the private anonymous memory."},
+    {"thp_stats", thp_stats, METH_NOARGS, "thp_stats() -> dict: the arena region's use."},
+    {"thp_child", [](PyObject*, PyObject*) -> PyObject* { thp_child(); Py_RETURN_NONE; }, METH_NOARGS,
+     "thp_child(): after a fork outside serve(): new arenas on small pages."},
     {nullptr, nullptr, 0, nullptr},
 };
 
