@@ -208,8 +208,8 @@ def main() -> None:
     if native is not None:
         # the per-request loop runs in C (csrc/zygote/zygote_loop.cpp); Python
         # runs again only in a forked child, handed its spawn line
-        line = native.serve(chan.fileno())
-        if line is None:
+        got = native.serve(chan.fileno())
+        if got is None:
             return  # channel closed / SIGTERM: the loop killed its sandboxes
         chan.detach()  # the loop closed the descriptor in the child
         if debug:
@@ -217,7 +217,10 @@ def main() -> None:
         import random
 
         random.seed()  # what os.fork's after-fork handler would have done
-        worker.worker_main(json.loads(line))  # never returns
+        if isinstance(got, tuple):
+            worker.worker_main_booted(got)  # bootstrapped in C; never returns
+        else:
+            worker.worker_main(json.loads(got))  # never returns
         os._exit(70)
 
     rfd, wfd = os.pipe()

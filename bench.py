@@ -143,6 +143,59 @@ def cpu_usage_s():
     return (sum(v) - v[3] - v[4]) / os.sysconf("SC_CLK_TCK"), "procstat"
 
 
+def _proc_times(pid: int):
+    """(own CPU s, reaped children's CPU s) of a process, from /proc/<pid>/stat."""
+    with open(f"/proc/{pid}/stat") as f:
+        fields = f.read().rsplit(")", 1)[1].split()
+    tck = os.sysconf("SC_CLK_TCK")
+    return (int(fields[11]) + int(fields[12])) / tck, (int(fields[13]) + int(fields[14])) / tck
+
+
+def _children(pid: int):
+    out = []
+    try:
+        for tid in os.listdir(f"/proc/{pid}/task"):
+            with open(f"/proc/{pid}/task/{tid}/children") as f:
+                out.extend(int(x) for x in f.read().split())
+    except OSError:
+        pass
+    return out
+
+
+def cpu_by_role(service_pid):
+    """CPU seconds so far of the service's processes by role: front-end
+    replicas, executor daemons (+ their kernel broker threads), zygotes (the
+    forks) and sandboxes (reaped children of the zygotes; live ones count
+    once reaped), plus this bench process and its load generators."""
+    roles = {"frontend": 0.0, "executor_daemon": 0.0, "zygote": 0.0, "sandboxes": 0.0, "bench_clients": 0.0}
+    t = os.times()
+    roles["bench_clients"] = t.user + t.system + t.children_user + t.children_system
+    if service_pid is None:
+        return roles
+    stack, seen = [service_pid], set()
+    while stack:
+        pid = stack.pop()
+        if pid in seen:
+            continue
+        seen.add(pid)
+        try:
+            with open(f"/proc/{pid}/cmdline", "rb") as f:
+                cmd = f.read()
+            own, reaped = _proc_times(pid)
+        except OSError:
+            continue
+        if b"bee-executor" in cmd:
+            roles["executor_daemon"] += own + reaped
+            stack.extend(_children(pid))
+        elif b"zygote" in cmd:
+            roles["zygote"] += own
+            roles["sandboxes"] += reaped  # live sandboxes: counted when reaped
+        else:
+            roles["frontend"] += own + reaped
+            stack.extend(_children(pid))
+    return roles
+
+
 def free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -291,10 +344,14 @@ def run_loadgens(n_procs, targets, source, concurrency, warmup, steps, sync, mar
     sync()
     if marks is not None:
         marks["t0"], marks["cpu0"] = time.perf_counter(), cpu_usage_s()[0]
+        marks["roles0"] = cpu_by_role(marks.get("svc"))
     out = [results.get(timeout=3600) for _ in procs]
     sync()
     for p in procs:
         p.join(timeout=30)
+    if marks is not None:
+        # (after the join: the load generators' CPU is then in our children's)
+        marks["roles1"] = cpu_by_role(marks.get("svc"))
     return out
 
 
@@ -400,20 +457,24 @@ def main():
         loadgens = n_gpus if world == 1 and n_gpus > 1 else 1
 
         cpu0, cpu_src = cpu_usage_s()
+        svc_pid = proc.pid if proc is not None else None
         if loadgens > 1:
-            marks = {}
+            marks = {"roles0": None, "svc": svc_pid}
             gathered = run_loadgens(loadgens, targets, source, args.concurrency, args.warmup, args.steps, barrier, marks)
             elapsed = max(g[0] for g in gathered)
             cpu_busy = (cpu_usage_s()[0] - marks["cpu0"]) / max(time.perf_counter() - marks["t0"], 1e-9)
+            roles0, roles1 = marks["roles0"], marks.get("roles1")
         else:
             loop.run_until_complete(run_clients(targets, first, source, args.concurrency, args.warmup))  # warm every pool
             barrier()
             cpu0, cpu_src = cpu_usage_s()
+            roles0 = cpu_by_role(svc_pid)
             t0 = time.perf_counter()
             lat, errors, exec_times, phases = loop.run_until_complete(
                 run_clients(targets, first, source, args.concurrency, args.steps))
             barrier()
             elapsed = time.perf_counter() - t0
+            roles1 = cpu_by_role(svc_pid)
             cpu_busy = (cpu_usage_s()[0] - cpu0) / elapsed if elapsed > 0 else 0.0
             gathered = [(elapsed, lat, errors, exec_times, phases)]
             if world > 1:
@@ -511,6 +572,12 @@ def main():
                 out["gang_allreduce"] = gang
             out["executors"] = executor_stats(hport)
             out["cpu_cores_busy"] = {"value": round(cpu_busy, 2), "source": cpu_src}
+            if roles0 is not None and roles1 is not None and total:
+                # CPU per Execute by role over the timed region (rank 0's node)
+                per = {k: round((roles1[k] - roles0[k]) * 1e3 / total, 3) for k in roles0}
+                per["all_cgroup"] = round(cpu_busy * max_elapsed * 1e3 / total, 3)
+                per["unattributed"] = round(per["all_cgroup"] - sum(v for k, v in per.items() if k != "all_cgroup"), 3)
+                out["cpu_ms_per_exec"] = per
             print(json.dumps(out), flush=True)
         if world > 1:
             dist.barrier()
