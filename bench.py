@@ -417,6 +417,33 @@ def executor_stats(hport):
         return repr(e)[:200]
 
 
+def wait_pools_ready(hport, timeout_s=240.0):
+    """Steady state before timing: every slot's direct (torch) and light
+    (pandas) pools at target, all zygotes up.  Their start-up (interpreter
+    imports, huge-page collapse, HIP warm-up of direct sandboxes) is one-time
+    CPU that would otherwise land inside the timed region."""
+    import urllib.request
+
+    deadline = time.monotonic() + timeout_s
+    while time.monotonic() < deadline:
+        try:
+            with urllib.request.urlopen(f"http://127.0.0.1:{hport}/v1/status", timeout=10) as f:
+                st = json.load(f)
+            ready = True
+            for s in st["slots"]:
+                e = s["executor"]
+                if e.get("zygotes_alive", 0) < e.get("zygotes", 0) or e.get("ready_direct", 0) < e.get("target", 0) or \
+                        e.get("ready_light", 0) < e.get("light_target", 0):
+                    ready = False
+            if ready:
+                time.sleep(0.5)
+                return True
+        except Exception:  # noqa: BLE001
+            pass
+        time.sleep(0.25)
+    return False
+
+
 def main():
     args = parse_args()
     world, rank, local = dist_env()
@@ -456,6 +483,10 @@ def main():
         # load generator each; a single-process N-GPU run starts N of them.
         loadgens = n_gpus if world == 1 and n_gpus > 1 else 1
 
+        if rank == 0:
+            wait_pools_ready(hport)
+        if world > 1:
+            dist.barrier()
         cpu0, cpu_src = cpu_usage_s()
         svc_pid = proc.pid if proc is not None else None
         if loadgens > 1:

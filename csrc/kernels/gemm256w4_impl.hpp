@@ -80,6 +80,11 @@ enum : int {
   kGroup2 = 128,
   kGroup8 = 256,
   kGroup16 = 512,
+  // any M, N (K still a multiple of 64): ceil-div grid, each operand panel's
+  // descriptor bounded by the rows that exist (the rest read as zero), and
+  // blocks on the ragged border -- or any block when ldc breaks the vector
+  // stores' alignment -- store element by element under a mask
+  kEdge = 1024,
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
@@ -107,14 +112,17 @@ struct Panel {
   int row_bytes;    // ld * 2
 };
 
-__device__ __forceinline__ Panel make_panel(const uint16_t* base, int ld, int lane) {
+__device__ __forceinline__ Panel make_panel(const uint16_t* base, int ld, int lane, int rows = 256) {
   Panel p;
   // descriptor inputs readfirstlane'd so the compiler can PROVE the SRD
   // uniform (else it wraps every load in a waterfall loop: guide T20)
   const uint64_t addr = (uint64_t)base;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)addr);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32));
-  const int64_t span = (int64_t)256 * ld * 2;  // integer clamp (HIP's min() has no int64 overload: it went through f64)
+  // `rows` (< 256 on the ragged border) bounds the panel: the last real row
+  // ends at (rows-1)*ld*2 + K*2 <= rows*ld*2, every row past it is out of
+  // range and loads zeros
+  const int64_t span = (int64_t)rows * ld * 2;  // integer clamp (HIP's min() has no int64 overload: it went through f64)
   const uint32_t bytes = __builtin_amdgcn_readfirstlane(span > 0xffffffffll ? 0xffffffffu : (uint32_t)span);
   p.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
   p.row_bytes = ld * 2;
@@ -316,6 +324,49 @@ __device__ __forceinline__ void epilogue(uint16_t* smem, const f32x4 (&acc)[8][8
   }
 }
 
+// kEdge border blocks: the same LDS staging, element stores under the
+// (row < M, col < N) mask; no alignment assumed of C or ldc
+template <bool OUT_BF16>
+__device__ __forceinline__ void epilogue_masked(uint16_t* smem, const f32x4 (&acc)[8][8], void* __restrict__ C,
+                                                int ldc, int64_t row0, int col0, int M, int N, int wave, int lane,
+                                                float alpha, float beta) {
+  float* ep = reinterpret_cast<float*>(smem) + wave * kEpWaveFloats;
+#pragma unroll
+  for (int half = 0; half < 4; ++half) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          ep[(ii * 16 + (lane >> 4) * 4 + r) * kEpPitch + j * 16 + (lane & 15)] = alpha * acc[half * 2 + ii][j][r];
+    const int64_t grow0 = row0 + half * 32;
+    // 64 lanes x 2 columns per row, one row per pass: consecutive lanes,
+    // consecutive addresses
+#pragma unroll 4
+    for (int row = 0; row < kEpRows; ++row) {
+      const int64_t grow = grow0 + row;
+      if (grow >= M) break;  // wave-uniform
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int col = e * 64 + lane;
+        const int gcol = col0 + col;
+        if (gcol >= N) continue;
+        float v = ep[row * kEpPitch + col];
+        if constexpr (OUT_BF16) {
+          uint16_t* dst = (uint16_t*)C + grow * ldc + gcol;
+          if (beta != 0.f) v += beta * bf16_bits_to_float(*dst);
+          *dst = float_to_bf16_bits(v);
+        } else {
+          float* dst = (float*)C + grow * ldc + gcol;
+          if (beta != 0.f) v += beta * *dst;
+          *dst = v;
+        }
+      }
+    }
+  }
+}
+
 template <bool OUT_BF16, int O>
 __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t* __restrict__ A,
                                                                   const uint16_t* __restrict__ Bt,
@@ -325,7 +376,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   constexpr bool pin = (O & kPinOrder) != 0, inter = (O & kInterleave) != 0, am = (O & kAsmMfma) != 0,
                  early = (O & kEarlyGlds) != 0, reads_early = (O & kReadsEarly) != 0;
 
-  const int nbm = M / TM, nbn = N / TN, nblocks = nbm * nbn;
+  constexpr bool edge = (O & kEdge) != 0;
+  const int nbm = edge ? (M + TM - 1) / TM : M / TM, nbn = edge ? (N + TN - 1) / TN : N / TN, nblocks = nbm * nbn;
   const int b = xcd_remap(blockIdx.x, nblocks);
   constexpr int kGm = (O & kGroup2) ? 2 : (O & kGroup8) ? 8 : (O & kGroup16) ? 16 : kGroupM;
   const int group = kGm * nbn;
@@ -337,8 +389,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 1, wc = wave & 1;
-  const Panel pa = make_panel(A + (int64_t)m0 * lda, lda, lane);
-  const Panel pb = make_panel(Bt + (int64_t)n0 * ldb, ldb, lane);
+  const Panel pa = make_panel(A + (int64_t)m0 * lda, lda, lane, edge ? min(TM, M - m0) : TM);
+  const Panel pb = make_panel(Bt + (int64_t)n0 * ldb, ldb, lane, edge ? min(TN, N - n0) : TN);
 
   f32x4 acc[8][8];
 #pragma unroll
@@ -431,6 +483,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
           if constexpr (OUT_BF16) ((uint16_t*)C)[row * ldc + col] = float_to_bf16_bits(alpha * acc[i][j][r]);
           else ((float*)C)[row * ldc + col] = alpha * acc[i][j][r] + (beta != 0.f ? beta * ((float*)C)[row * ldc + col] : 0.f);
         }
+  } else if (edge && (m0 + TM > M || n0 + TN > N || (ldc % (OUT_BF16 ? 8 : 4)) != 0 ||
+                      ((uintptr_t)C & 15) != 0)) {
+    epilogue_masked<OUT_BF16>(smem, acc, C, ldc, m0 + wr * 128, n0 + wc * 128, M, N, wave, lane, alpha, beta);
   } else {
     epilogue<OUT_BF16>(smem, acc, C, ldc, m0 + wr * 128, n0 + wc * 128, wave, lane, alpha, beta);
   }
@@ -445,10 +500,17 @@ inline bool ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16) {
          ldc % (out_bf16 ? 8 : 4) == 0 && span_ok(lda) && span_ok(ldb);
 }
 
+// kEdge: any M, N; the rest as ok()
+inline bool edge_ok(int M, int N, int K, int lda, int ldb) {
+  const auto span_ok = [K](int ld) { return (int64_t)256 * ld * 2 + (int64_t)K * 2 < 0x7fffffffll; };
+  return M > 0 && N > 0 && K > 0 && K % TK == 0 && lda % 8 == 0 && ldb % 8 == 0 && span_ok(lda) && span_ok(ldb);
+}
+
 template <int O>
 inline void launch(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
                    float beta, bool out_bf16, hipStream_t stream) {
-  const unsigned grid = (unsigned)((M / TM) * (N / TN));
+  const unsigned grid = (O & kEdge) ? (unsigned)(((M + TM - 1) / TM) * ((N + TN - 1) / TN))
+                                    : (unsigned)((M / TM) * (N / TN));
   if (out_bf16)
     gemm_bf16_tn_256w4<true, O><<<grid, kThreads, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N, K,
                                                                lda, ldb, ldc, alpha, beta);

@@ -467,6 +467,9 @@ __global__ __launch_bounds__(256) void transpose_wide_scalar(const T* __restrict
 bool gemm256_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16);  // gemm_bf16_256.hip
 void launch_gemm256(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
                     float beta, bool out_bf16, hipStream_t stream, int which);
+bool gemm256_edge_ok(int M, int N, int K, int lda, int ldb);
+void launch_gemm256_edge(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                         float alpha, float beta, bool out_bf16, hipStream_t stream);
 
 }  // namespace bk
 
@@ -491,8 +494,19 @@ static bool edge_ok(int M, int N, int K, int lda, int ldb) {
 // Shapes that are not tile multiples take the edge kernel (128x128 tiles,
 // zero-filling buffer loads, masked stores) when K and the leading
 // dimensions are multiples of 8; only the rest reach the generic kernel.
+// Large non-tile-multiple shapes with K a multiple of 64 take the 4-wave
+// 256x256 kernel in its edge mode (variant 7) when they fill the chip.
 // variant: 0 = auto, 1 = generic, 2 = 128x128, 3 = 256x256 (4-wave or 8-wave
-// by K), 4 = 256x256 8-wave, 5 = 256x256 4-wave, 6 = 128x128 edge (benchmarks, tests).
+// by K), 4 = 256x256 8-wave, 5 = 256x256 4-wave, 6 = 128x128 edge, 7 = 256x256
+// 4-wave edge (benchmarks, tests).
+static int auto_variant(bool ok256, bool ok128, bool okedge, bool ok256e, int M, int N) {
+  const int64_t tiles256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
+  if (ok256 && (M / 256) * (N / 256) >= 128) return 3;
+  if (ok128) return 2;
+  if (ok256e && tiles256 >= 128) return 7;
+  return okedge ? 6 : 1;
+}
+
 BK_API int bk_gemm_bf16_tn_variant(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb,
                                    int ldc, float alpha, float beta, int out_dtype, int variant, hipStream_t stream) {
   if (!A || !Bt || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N) return kBadArgument;
@@ -501,12 +515,15 @@ BK_API int bk_gemm_bf16_tn_variant(const void* A, const void* Bt, void* C, int M
   const bool ok128 = al && bk_gemm_bf16_fast_ok(M, N, K, lda, ldb);
   const bool ok256 = al && aligned16(C) && gemm256_ok(M, N, K, lda, ldb, ldc, out_dtype == kBF16);
   const bool okedge = al && edge_ok(M, N, K, lda, ldb);
-  if (variant == 0) variant = (ok256 && (M / 256) * (N / 256) >= 128) ? 3 : ok128 ? 2 : okedge ? 6 : 1;
+  const bool ok256e = al && gemm256_edge_ok(M, N, K, lda, ldb);
+  if (variant == 0) variant = auto_variant(ok256, ok128, okedge, ok256e, M, N);
   if ((variant >= 3 && variant <= 5 && !ok256) || (variant == 2 && !ok128) || (variant == 6 && !okedge) ||
-      variant < 1 || variant > 6)
+      (variant == 7 && !ok256e) || variant < 1 || variant > 7)
     return kBadArgument;
   const bool bf = out_dtype == kBF16;
-  if (variant == 6) {
+  if (variant == 7) {
+    launch_gemm256_edge(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, bf, stream);
+  } else if (variant == 6) {
     const unsigned grid = (unsigned)(((M + BM - 1) / BM) * ((N + BN - 1) / BN));
     if (bf)
       gemm_bf16_tn_edge<true><<<grid, kGemmThreads, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N, K,
@@ -542,7 +559,7 @@ BK_API int bk_gemm_bf16_pick(const void* A, const void* Bt, const void* C, int M
   const bool al = aligned16(A) && aligned16(Bt);
   const bool ok128 = al && bk_gemm_bf16_fast_ok(M, N, K, lda, ldb);
   const bool ok256 = al && aligned16(C) && gemm256_ok(M, N, K, lda, ldb, ldc, out_dtype == kBF16);
-  return (ok256 && (M / 256) * (N / 256) >= 128) ? 3 : ok128 ? 2 : (al && edge_ok(M, N, K, lda, ldb)) ? 6 : 1;
+  return auto_variant(ok256, ok128, al && edge_ok(M, N, K, lda, ldb), al && gemm256_edge_ok(M, N, K, lda, ldb), M, N);
 }
 
 // C = alpha * A . Bt^T + beta * C.  out_dtype: kBF16 or kF32.

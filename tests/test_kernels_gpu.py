@@ -345,8 +345,10 @@ def test_gemm_edge_kernel_unaligned_shapes(gpu, shape, out):
     c0 = torch.empty(M, ldc, device="cuda", dtype=dt).uniform_(-1, 1, generator=g)
     c = c0.clone()
     lib = _native.lib()
+    # K % 64 == 0 and enough 256^2 tiles: the 4-wave kernel's edge mode (7); else the 128^2 edge kernel (6)
+    want = 7 if K % 64 == 0 and ((M + 255) // 256) * ((N + 255) // 256) >= 128 else 6
     assert lib.bk_gemm_bf16_pick(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, ldc,
-                                 0 if out == "float32" else 2) == 6
+                                 0 if out == "float32" else 2) == want
     rc = lib.bk_gemm_bf16_tn_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, ldc, 0.75, 0.5,
                                      0 if out == "float32" else 2, 0, torch.cuda.current_stream().cuda_stream)
     assert rc == 0
@@ -385,7 +387,54 @@ def test_gemm_huge_leading_dimension(gpu):
     del store
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("shape", [(257, 300, 64), (4095, 4097, 4096), (600, 256, 512), (256, 1000, 128), (1, 1, 64)])
+@pytest.mark.parametrize("out", ["float32", "bfloat16"])
+@pytest.mark.parametrize("c_offset", [0, 1])
+def test_gemm_256_edge_mode(gpu, shape, out, c_offset):
+    """The 4-wave 256^2 kernel in edge mode (variant 7): operand panels
+    bounded by the rows that exist, masked element stores on the ragged
+    border and wherever C / ldc break 16-B alignment (odd ldc, C offset by
+    one element) -- against fp64, beta epilogue, padding intact."""
+    import torch
+
+    from bee_code_interpreter_fs_amd.ops import _native
+
+    M, N, K = shape
+    ldc = N + 3  # odd: no vector store is ever aligned
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + c_offset)
+    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    bt = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    dt = torch.float32 if out == "float32" else torch.bfloat16
+    store0 = torch.empty(M * ldc + 8, device="cuda", dtype=dt).uniform_(-1, 1, generator=g)
+    store = store0.clone()
+    c = store[c_offset : c_offset + M * ldc].view(M, ldc)
+    c0 = store0[c_offset : c_offset + M * ldc].view(M, ldc)
+    rc = _native.lib().bk_gemm_bf16_tn_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, ldc, 0.75,
+                                               0.5, 0 if out == "float32" else 2, 7,
+                                               torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = 0.75 * (a.double() @ bt.double().T) + 0.5 * c0[:, :N].double()
+    tol = 1e-3 if out == "float32" else 4e-2
+    assert (c[:, :N].double() - ref).abs().max().item() < tol * max(1.0, ref.abs().max().item())
+    assert torch.equal(c[:, N:], c0[:, N:])
+    assert torch.equal(store[:c_offset], store0[:c_offset]) and torch.equal(store[c_offset + M * ldc:],
+                                                                          store0[c_offset + M * ldc:])
+
+
+def test_gemm_256_edge_mode_refuses_ragged_k(gpu):
+    import torch
+
+    from bee_code_interpreter_fs_amd.ops import _native
+
+    a = torch.zeros(300, 100, device="cuda", dtype=torch.bfloat16)
+    c = torch.zeros(300, 300, device="cuda", dtype=torch.float32)
+    rc = _native.lib().bk_gemm_bf16_tn_variant(a.data_ptr(), a.data_ptr(), c.data_ptr(), 300, 300, 100, 100, 100, 300,
+                                               1.0, 0.0, 0, 7, torch.cuda.current_stream().cuda_stream)
+    assert rc == 1  # kBadArgument: K % 64 != 0 is the 128^2 edge kernel's
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("out", ["float32", "bfloat16"])
 def test_gemm_kernel_variants_with_beta(gpu, variant, out):
     """Every GEMM kernel (generic / 128^2 / 256^2 by shape / 256^2 8-wave
