@@ -80,10 +80,11 @@ enum : int {
   kGroup2 = 128,
   kGroup8 = 256,
   kGroup16 = 512,
-  // any M, N (K still a multiple of 64): ceil-div grid, each operand panel's
-  // descriptor bounded by the rows that exist (the rest read as zero), and
-  // blocks on the ragged border -- or any block when ldc breaks the vector
-  // stores' alignment -- store element by element under a mask
+  // any M, N, and K % 8 == 0: ceil-div grid, each operand panel's descriptor
+  // bounded by the rows that exist (the rest read as zero), chunks past K in
+  // the last K-tile read as zero, and blocks on the ragged border -- or any
+  // block when ldc breaks the vector stores' alignment -- store element by
+  // element under a mask
   kEdge = 1024,
 };
 
@@ -110,9 +111,10 @@ struct Panel {
   __amdgpu_buffer_rsrc_t rsrc;
   int lane_off[2];  // bytes: (lane/8) rows + this lane's swizzled 16-B chunk, for even / odd i
   int row_bytes;    // ld * 2
+  int k_lim[2];     // kEdge: this lane's chunk holds K columns while k0 < k_lim (K - 8 * chunk)
 };
 
-__device__ __forceinline__ Panel make_panel(const uint16_t* base, int ld, int lane, int rows = 256) {
+__device__ __forceinline__ Panel make_panel(const uint16_t* base, int ld, int lane, int rows = 256, int K = 0) {
   Panel p;
   // descriptor inputs readfirstlane'd so the compiler can PROVE the SRD
   // uniform (else it wraps every load in a waterfall loop: guide T20)
@@ -131,18 +133,28 @@ __device__ __forceinline__ Panel make_panel(const uint16_t* base, int ld, int la
   for (int par = 0; par < 2; ++par) {
     const int c = (lane & 7) ^ ((par * 4 + (lane >> 4)) & 7);
     p.lane_off[par] = (lane >> 3) * ld * 2 + c * 16;
+    p.k_lim[par] = K - c * 8;
   }
   return p;
 }
 
+// a lane's 16-B chunk at column k0 + 8 * chunk: past K (the ragged last
+// K-tile of kEdge) its offset becomes 2^31, beyond every panel's extent, and
+// the load returns zeros.  (K % 8 == 0: chunks are all in or all out.)
+// (kt is a compile-time constant at every call: the select folds away
+// when false)
+__device__ __forceinline__ int chunk_off(const Panel& p, int k0, int par, bool kt) {
+  return (kt && k0 >= p.k_lim[par]) ? (int)0x80000000 : p.lane_off[par];
+}
+
 // stage one operand's K-tile: 8 wave-instructions of 1 KiB (8 rows) each;
 // `wave` must be wave-uniform (readfirstlane'd) so the LDS base goes to M0
-__device__ __forceinline__ void stage(const Panel& p, int k0, uint16_t* lds_operand, int wave) {
+__device__ __forceinline__ void stage(const Panel& p, int k0, uint16_t* lds_operand, int wave, bool kt = false) {
 #pragma unroll
   for (int i = 0; i < kGlds; ++i) {
     const int soff = (wave * 64 + i * 8) * p.row_bytes + k0 * 2;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(p.rsrc, (lds_void_ptr)(lds_operand + (wave * kGlds + i) * 8 * TK), 16,
-                                             p.lane_off[i & 1], soff, 0, 0);
+                                             chunk_off(p, k0, i & 1, kt), soff, 0, 0);
   }
 }
 
@@ -202,10 +214,11 @@ __device__ __forceinline__ void mfma_asm(f32x4& acc, const bf16x8& a, const bf16
 }
 
 // the i-th of one operand's 8 K-tile glds (stage() split up)
-__device__ __forceinline__ void glds_one(const Panel& p, int k0, uint16_t* lds_operand, int wave, int i) {
+__device__ __forceinline__ void glds_one(const Panel& p, int k0, uint16_t* lds_operand, int wave, int i,
+                                         bool kt = false) {
   const int soff = (wave * 64 + i * 8) * p.row_bytes + k0 * 2;
   __builtin_amdgcn_raw_ptr_buffer_load_lds(p.rsrc, (lds_void_ptr)(lds_operand + (wave * kGlds + i) * 8 * TK), 16,
-                                           p.lane_off[i & 1], soff, 0, 0);
+                                           chunk_off(p, k0, i & 1, kt), soff, 0, 0);
 }
 
 // One K-tile of the kAsmMfma|kInterleave schedule, in 2 x 16 groups fenced by
@@ -217,7 +230,7 @@ __device__ __forceinline__ void glds_one(const Panel& p, int k0, uint16_t* lds_o
 // A ds_read overwrites a fragment register >= 16 MFMAs after its last reader
 // (WAR on srcA/B of an in-flight MFMA, invisible to the hazard recognizer
 // through inline asm).
-template <bool INIT, bool EARLY, bool READS_EARLY>
+template <bool INIT, bool EARLY, bool READS_EARLY, bool KT = false>
 __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8], bf16x8 (&fa1)[8],
                                           bf16x8 (&fb1)[8], uint16_t* smem, const Panel& pa, const Panel& pb, int t,
                                           int nk, int wr, int wc, int lane, int wave) {
@@ -256,12 +269,12 @@ __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], 
     for (int jj = 0; jj < 4; ++jj) mfma_asm<false>(acc[g >> 1][(g & 1) * 4 + jj], fa1[g >> 1], fb1[(g & 1) * 4 + jj]);
     if constexpr (EARLY) {  // all 16 glds in the first 8 groups: more time to land
       if (g < 8) {
-        glds_one(pa, kn, cur, wave, g);
-        glds_one(pb, kn, cur + kOperand, wave, g);
+        glds_one(pa, kn, cur, wave, g, KT);
+        glds_one(pb, kn, cur + kOperand, wave, g, KT);
       }
     } else {
-      if (g < 8) glds_one(pa, kn, cur, wave, g);
-      else glds_one(pb, kn, cur + kOperand, wave, g - 8);
+      if (g < 8) glds_one(pa, kn, cur, wave, g, KT);
+      else glds_one(pb, kn, cur + kOperand, wave, g - 8, KT);
     }
     // in the order the next K-tile's first groups consume them: fa0[0],
     // fb0[0..7], fa0[1..7]
@@ -389,8 +402,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 1, wc = wave & 1;
-  const Panel pa = make_panel(A + (int64_t)m0 * lda, lda, lane, edge ? min(TM, M - m0) : TM);
-  const Panel pb = make_panel(Bt + (int64_t)n0 * ldb, ldb, lane, edge ? min(TN, N - n0) : TN);
+  const Panel pa = make_panel(A + (int64_t)m0 * lda, lda, lane, edge ? min(TM, M - m0) : TM, K);
+  const Panel pb = make_panel(Bt + (int64_t)n0 * ldb, ldb, lane, edge ? min(TN, N - n0) : TN, K);
 
   f32x4 acc[8][8];
 #pragma unroll
@@ -398,13 +411,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / TK;
+  const int nk = edge ? (K + TK - 1) / TK : K / TK;  // kEdge: a ragged last K-tile reads zeros past K
   // prologue: tiles 0 and 1 in flight, wait for tile 0 (16 glds per tile)
-  stage(pa, 0, smem, wave);
-  stage(pb, 0, smem + kOperand, wave);
+  stage(pa, 0, smem, wave, edge);
+  stage(pb, 0, smem + kOperand, wave, edge);
   if (nk > 1) {
-    stage(pa, TK, smem + kBuf, wave);
-    stage(pb, TK, smem + kBuf + kOperand, wave);
+    stage(pa, TK, smem + kBuf, wave, edge);
+    stage(pb, TK, smem + kBuf + kOperand, wave, edge);
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -416,8 +429,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
     // hand-interleaved pipeline; K-tile 0 peeled so its MFMAs start the
     // accumulators from the constant 0 (no AGPR zero-fill to fence)
     read_frags(smem, wr, wc, lane, 0, fa0, fb0);
-    ktile_asm<true, early, reads_early>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
-    for (int t = 1; t < nk; ++t) ktile_asm<false, early, reads_early>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
+    ktile_asm<true, early, reads_early, edge>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
+    for (int t = 1; t < nk; ++t) ktile_asm<false, early, reads_early, edge>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
   } else if constexpr ((O & kNoCarry) != 0) {
     // loop-carried state is the accumulators only (simpler register
     // allocation); the first MFMAs of each K-tile wait for its first reads
@@ -430,8 +443,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       barrier();
       const int kn = min(t + 2, nk - 1) * TK;
-      stage(pa, kn, cur, wave);
-      stage(pb, kn, cur + kOperand, wave);
+      stage(pa, kn, cur, wave, edge);
+      stage(pb, kn, cur + kOperand, wave, edge);
     }
   } else {
   read_frags(smem, wr, wc, lane, 0, fa0, fb0);
@@ -452,8 +465,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
     // the end, re-stage the last K-tile into the buffer nobody reads again
     // and read fragments nobody uses
     const int kn = min(t + 2, nk - 1) * TK;
-    stage(pa, kn, cur, wave);
-    stage(pb, kn, cur + kOperand, wave);
+    stage(pa, kn, cur, wave, edge);
+    stage(pb, kn, cur + kOperand, wave, edge);
     read_frags(nxt, wr, wc, lane, 0, fa0, fb0);
     if constexpr (inter) interleave_hint<16, 16>();
     else if constexpr (pin) __builtin_amdgcn_sched_barrier(0);
@@ -503,7 +516,7 @@ inline bool ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16) {
 // kEdge: any M, N; the rest as ok()
 inline bool edge_ok(int M, int N, int K, int lda, int ldb) {
   const auto span_ok = [K](int ld) { return (int64_t)256 * ld * 2 + (int64_t)K * 2 < 0x7fffffffll; };
-  return M > 0 && N > 0 && K > 0 && K % TK == 0 && lda % 8 == 0 && ldb % 8 == 0 && span_ok(lda) && span_ok(ldb);
+  return M > 0 && N > 0 && K > 0 && K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && span_ok(lda) && span_ok(ldb);
 }
 
 template <int O>

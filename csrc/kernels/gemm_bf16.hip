@@ -258,6 +258,80 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_edge(const uint1
       }
 }
 
+// ---- skinny strip: C[:, 0:r] for r <= 16 columns -------------------------------
+// What is left right of the 256-multiples when N % 256 is tiny (4097 = 16 *
+// 256 + 1): a GEMV-shaped sliver whose cost is reading A once.  One wave per
+// two rows of A, 16-B chunks (64 lanes x 8 = 512 K-columns per step), the r
+// rows of Bt from L2, f32 FMAs, a cross-lane sum per output.
+constexpr int kSkinnyCols = 16, kSkinnyRows = 2;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(256) void gemm_bf16_tn_skinny(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bt,
+                                                           void* __restrict__ C, int M, int r, int K, int lda, int ldb,
+                                                           int ldc, float alpha, float beta) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * kSkinnyRows;
+  if (row0 >= M) return;  // whole wave
+  float acc[kSkinnyRows][kSkinnyCols];
+#pragma unroll
+  for (int i = 0; i < kSkinnyRows; ++i)
+#pragma unroll
+    for (int j = 0; j < kSkinnyCols; ++j) acc[i][j] = 0.f;
+  for (int k = lane * 8; k < K; k += 512) {  // K % 8 == 0: chunks are whole
+    float a[kSkinnyRows][8];
+#pragma unroll
+    for (int i = 0; i < kSkinnyRows; ++i) {
+      const int64_t row = min(row0 + i, (int64_t)M - 1);  // (a clamped duplicate row is never stored)
+      const uint4 q = *reinterpret_cast<const uint4*>(A + row * lda + k);
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[i][2 * e] = bf16_bits_to_float((uint16_t)(w[e] & 0xffff));
+        a[i][2 * e + 1] = bf16_bits_to_float((uint16_t)(w[e] >> 16));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kSkinnyCols; ++j) {
+      if (j >= r) break;
+      const uint4 q = *reinterpret_cast<const uint4*>(Bt + (int64_t)j * ldb + k);
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float b0 = bf16_bits_to_float((uint16_t)(w[e] & 0xffff)), b1 = bf16_bits_to_float((uint16_t)(w[e] >> 16));
+#pragma unroll
+        for (int i = 0; i < kSkinnyRows; ++i) acc[i][j] += a[i][2 * e] * b0 + a[i][2 * e + 1] * b1;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kSkinnyRows; ++i) {
+    const int64_t row = row0 + i;
+#pragma unroll
+    for (int j = 0; j < kSkinnyCols; ++j) {
+      if (j >= r) break;
+      const float s = wave_sum(acc[i][j]);
+      if (lane == 0 && row < M) {
+        float v = alpha * s;
+        if constexpr (OUT_BF16) {
+          uint16_t* c = (uint16_t*)C + row * ldc + j;
+          if (beta != 0.f) v += beta * bf16_bits_to_float(*c);
+          *c = float_to_bf16_bits(v);
+        } else {
+          float* c = (float*)C + row * ldc + j;
+          if (beta != 0.f) v += beta * *c;
+          *c = v;
+        }
+      }
+    }
+  }
+}
+
 // ---- generic path ------------------------------------------------------------
 constexpr int GBM = 64, GBN = 64, GBK = 32;
 
@@ -494,8 +568,8 @@ static bool edge_ok(int M, int N, int K, int lda, int ldb) {
 // Shapes that are not tile multiples take the edge kernel (128x128 tiles,
 // zero-filling buffer loads, masked stores) when K and the leading
 // dimensions are multiples of 8; only the rest reach the generic kernel.
-// Large non-tile-multiple shapes with K a multiple of 64 take the 4-wave
-// 256x256 kernel in its edge mode (variant 7) when they fill the chip.
+// Large non-tile-multiple shapes take the 4-wave 256x256 kernel in its edge
+// mode (variant 7; K % 8 == 0) when they fill the chip.
 // variant: 0 = auto, 1 = generic, 2 = 128x128, 3 = 256x256 (4-wave or 8-wave
 // by K), 4 = 256x256 8-wave, 5 = 256x256 4-wave, 6 = 128x128 edge, 7 = 256x256
 // 4-wave edge (benchmarks, tests).
@@ -522,7 +596,38 @@ BK_API int bk_gemm_bf16_tn_variant(const void* A, const void* Bt, void* C, int M
     return kBadArgument;
   const bool bf = out_dtype == kBF16;
   if (variant == 7) {
-    launch_gemm256_edge(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, bf, stream);
+    // a remainder of <= 64 rows / columns past the 256-multiples would cost a
+    // whole extra wave of mostly-empty 256^2 tiles (4095 x 4097: 272 tiles on
+    // 256 CUs); it goes to the 128^2 edge kernel as a strip after the main
+    // block instead
+    const int es = bf ? 2 : 4;
+    const int rm = M % 256, rn = N % 256;
+    const int Mm = (rm && rm <= 64 && M > 256) ? M - rm : M;
+    const int Nm = (rn && rn <= 64 && N > 256) ? N - rn : N;
+    launch_gemm256_edge(A, Bt, C, Mm, Nm, K, lda, ldb, ldc, alpha, beta, bf, stream);
+    auto strip = [&](const void* a, const void* b, void* c, int m, int n) {
+      if (n <= kSkinnyCols) {  // a sliver of columns: read A once, GEMV-style
+        const unsigned g = (unsigned)((m + 4 * kSkinnyRows - 1) / (4 * kSkinnyRows));
+        if (bf)
+          gemm_bf16_tn_skinny<true><<<g, 256, 0, stream>>>((const uint16_t*)a, (const uint16_t*)b, c, m, n, K, lda, ldb,
+                                                           ldc, alpha, beta);
+        else
+          gemm_bf16_tn_skinny<false><<<g, 256, 0, stream>>>((const uint16_t*)a, (const uint16_t*)b, c, m, n, K, lda,
+                                                            ldb, ldc, alpha, beta);
+        return;
+      }
+      const unsigned grid = (unsigned)(((m + BM - 1) / BM) * ((n + BN - 1) / BN));
+      if (bf)
+        gemm_bf16_tn_edge<true><<<grid, kGemmThreads, 0, stream>>>((const uint16_t*)a, (const uint16_t*)b, c, m, n, K,
+                                                                   lda, ldb, ldc, alpha, beta);
+      else
+        gemm_bf16_tn_edge<false><<<grid, kGemmThreads, 0, stream>>>((const uint16_t*)a, (const uint16_t*)b, c, m, n, K,
+                                                                    lda, ldb, ldc, alpha, beta);
+    };
+    if (Nm < N)  // right strip, full height (the corner included)
+      strip(A, (const uint16_t*)Bt + (int64_t)Nm * ldb, (char*)C + (int64_t)Nm * es, M, N - Nm);
+    if (Mm < M)  // bottom strip left of it
+      strip((const uint16_t*)A + (int64_t)Mm * lda, Bt, (char*)C + (int64_t)Mm * ldc * es, M - Mm, Nm);
   } else if (variant == 6) {
     const unsigned grid = (unsigned)(((M + BM - 1) / BM) * ((N + BN - 1) / BN));
     if (bf)

@@ -346,7 +346,7 @@ def test_gemm_edge_kernel_unaligned_shapes(gpu, shape, out):
     c = c0.clone()
     lib = _native.lib()
     # K % 64 == 0 and enough 256^2 tiles: the 4-wave kernel's edge mode (7); else the 128^2 edge kernel (6)
-    want = 7 if K % 64 == 0 and ((M + 255) // 256) * ((N + 255) // 256) >= 128 else 6
+    want = 7 if ((M + 255) // 256) * ((N + 255) // 256) >= 128 else 6
     assert lib.bk_gemm_bf16_pick(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, ldc,
                                  0 if out == "float32" else 2) == want
     rc = lib.bk_gemm_bf16_tn_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, ldc, 0.75, 0.5,
@@ -387,7 +387,8 @@ def test_gemm_huge_leading_dimension(gpu):
     del store
 
 
-@pytest.mark.parametrize("shape", [(257, 300, 64), (4095, 4097, 4096), (600, 256, 512), (256, 1000, 128), (1, 1, 64)])
+@pytest.mark.parametrize("shape", [(257, 300, 64), (4095, 4097, 4096), (600, 256, 512), (256, 1000, 128), (1, 1, 64),
+                                   (4000, 4000, 4000), (300, 520, 72), (513, 260, 8), (1100, 1030, 136)])
 @pytest.mark.parametrize("out", ["float32", "bfloat16"])
 @pytest.mark.parametrize("c_offset", [0, 1])
 def test_gemm_256_edge_mode(gpu, shape, out, c_offset):
@@ -422,16 +423,16 @@ def test_gemm_256_edge_mode(gpu, shape, out, c_offset):
                                                                           store0[c_offset + M * ldc:])
 
 
-def test_gemm_256_edge_mode_refuses_ragged_k(gpu):
+def test_gemm_256_edge_mode_refuses_k_not_multiple_of_8(gpu):
     import torch
 
     from bee_code_interpreter_fs_amd.ops import _native
 
     a = torch.zeros(300, 100, device="cuda", dtype=torch.bfloat16)
     c = torch.zeros(300, 300, device="cuda", dtype=torch.float32)
-    rc = _native.lib().bk_gemm_bf16_tn_variant(a.data_ptr(), a.data_ptr(), c.data_ptr(), 300, 300, 100, 100, 100, 300,
+    rc = _native.lib().bk_gemm_bf16_tn_variant(a.data_ptr(), a.data_ptr(), c.data_ptr(), 300, 300, 99, 100, 100, 300,
                                                1.0, 0.0, 0, 7, torch.cuda.current_stream().cuda_stream)
-    assert rc == 1  # kBadArgument: K % 64 != 0 is the 128^2 edge kernel's
+    assert rc == 1  # kBadArgument: 16-B chunks need K % 8 == 0 (the generic kernel's case)
 
 
 @pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
