@@ -411,6 +411,8 @@ def executor_stats(hport):
             d = {k: round(e.get(k, 0), 3) for k in keys}
             n = max(e.get("executions", 0), 1)
             d["daemon_cpu_ms_per_exec"] = {k: round(v / n, 3) for k, v in (e.get("cpu_ms") or {}).items()}
+            # whole daemon lifetime (start-up included) by thread role
+            d["daemon_thread_cpu_ms_per_exec"] = {k: round(v / n, 3) for k, v in (e.get("thread_cpu_ms") or {}).items()}
             out.append(d)
         return out
     except Exception as e:  # noqa: BLE001

@@ -325,6 +325,7 @@ void KernelBroker::stop() {
 }
 
 void KernelBroker::accept_loop() {
+  ThreadRoleScope role(kThrAcceptor);
   while (!stopping_) {
     int fd = accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
     if (fd < 0) {
@@ -355,6 +356,7 @@ void KernelBroker::accept_loop() {
 }
 
 void KernelBroker::pool_thread() {
+  ThreadRoleScope role(kThrBrokerPool);
   std::unique_lock<std::mutex> lk(q_mu_);
   while (!stopping_) {
     if (queue_.empty()) {

@@ -260,6 +260,7 @@ void HttpServer::serve_forever() {
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
     active_++;
     std::thread([this, fd] {
+      ThreadRoleScope role(kThrHttp);
       handle_conn(fd);
       active_--;
     }).detach();

@@ -357,6 +357,7 @@ bool SandboxPool::any_zygote_alive() const {
 }
 
 void SandboxPool::zygote_reader(Zygote* z) {
+  ThreadRoleScope role(kThrZygoteReader);
   std::string buf, line;
   const int fd = z->fd;
   while (read_line(fd, buf, &line)) {
@@ -705,6 +706,7 @@ broker::Peer SandboxPool::peer_info(pid_t peer) {
 }
 
 void SandboxPool::worker_acceptor() {
+  ThreadRoleScope role(kThrAcceptor);
   while (!stopping_) {
     int fd = accept4(worker_listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
     if (fd < 0) {
@@ -725,6 +727,7 @@ void SandboxPool::worker_acceptor() {
 }
 
 void SandboxPool::worker_reader(int fd, pid_t peer) {
+  ThreadRoleScope role(kThrWorkerReader);
   std::string buf, line;
   std::shared_ptr<Worker> w;
   while (read_line(fd, buf, &line)) {
@@ -866,6 +869,7 @@ void SandboxPool::destroy(const std::shared_ptr<Worker>& w) {
 }
 
 void SandboxPool::cleanup_loop() {
+  ThreadRoleScope role(kThrCleanup);
   while (true) {
     std::string dir;
     {
@@ -972,6 +976,7 @@ int64_t SandboxPool::sandbox_vram_bytes(pid_t leader) {
 }
 
 void SandboxPool::watchdog_loop() {
+  ThreadRoleScope role(kThrWatchdog);
   while (!stopping_) {
     std::this_thread::sleep_for(std::chrono::milliseconds(cfg_.hbm_watchdog_ms));
     std::vector<std::shared_ptr<Worker>> running;
@@ -1413,6 +1418,9 @@ Json SandboxPool::status() {
   Json cpu = Json::object();
   for (int i = 0; i < kCpuParts; ++i) cpu.set(kCpuPartNames[i], g_cpu_ns[i].load() / 1e6);
   j.set("cpu_ms", cpu);
+  Json thr = Json::object();
+  for (auto& kv : thread_cpu_report()) thr.set(kv.first, kv.second);
+  j.set("thread_cpu_ms", thr);
   j.set("ready", (int64_t)(ready_[kDirect].size() + ready_[kLight].size() + ready_[kMin].size() + ready_[kMinCpu].size()));
   j.set("ready_min_cpu", (int64_t)ready_[kMinCpu].size());
   j.set("ready_min", (int64_t)ready_[kMin].size());

@@ -1,6 +1,8 @@
 #include "util.hpp"
 
 #include <dirent.h>
+#include <pthread.h>
+#include <sys/resource.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <ftw.h>
@@ -19,6 +21,73 @@ namespace bee {
 
 std::atomic<int64_t> g_cpu_ns[kCpuParts];
 const char* const kCpuPartNames[kCpuParts] = {"http", "worker_io", "zygote_io", "broker", "cleanup"};
+std::atomic<int64_t> g_thread_exit_ns[kThrRoles];
+// thread names (comm, <= 15 chars): what /proc/self/task/*/comm shows
+const char* const kThreadRoleNames[kThrRoles] = {"bee-http", "bee-wreader", "bee-zreader", "bee-broker",
+                                                 "bee-accept", "bee-cleanup", "bee-watchdog"};
+
+ThreadRoleScope::ThreadRoleScope(ThreadRole r) : role(r) { pthread_setname_np(pthread_self(), kThreadRoleNames[r]); }
+
+std::vector<std::pair<std::string, double>> thread_cpu_report() {
+  double roles[kThrRoles];
+  for (int i = 0; i < kThrRoles; ++i) roles[i] = g_thread_exit_ns[i].load() / 1e6;
+  double main_ms = 0, other_live = 0;
+  const long tck = sysconf(_SC_CLK_TCK);
+  const pid_t self = getpid();
+  if (DIR* d = opendir("/proc/self/task")) {
+    while (dirent* e = readdir(d)) {
+      if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+      char buf[512];
+      const std::string base = std::string("/proc/self/task/") + e->d_name;
+      const int fd = open((base + "/stat").c_str(), O_RDONLY | O_CLOEXEC);
+      if (fd < 0) continue;
+      const ssize_t n = read(fd, buf, sizeof buf - 1);
+      close(fd);
+      if (n <= 0) continue;
+      buf[n] = 0;
+      const char* open_paren = strchr(buf, '(');
+      const char* close_paren = strrchr(buf, ')');
+      if (!open_paren || !close_paren) continue;
+      const std::string comm(open_paren + 1, close_paren);
+      unsigned long ut = 0, st = 0;
+      // fields after ')': state(3) ... utime(14) stime(15)
+      const char* p = close_paren + 2;
+      int field = 3;
+      while (*p && field < 14) {
+        if (*p == ' ') ++field;
+        ++p;
+      }
+      if (sscanf(p, "%lu %lu", &ut, &st) != 2) continue;
+      const double ms = (ut + st) * 1000.0 / tck;
+      if (atoi(e->d_name) == self) {
+        main_ms += ms;
+        continue;
+      }
+      bool found = false;
+      for (int i = 0; i < kThrRoles; ++i)
+        if (comm == kThreadRoleNames[i]) {
+          roles[i] += ms;
+          found = true;
+        }
+      if (!found) other_live += ms;
+    }
+    closedir(d);
+  }
+  rusage ru{};
+  getrusage(RUSAGE_SELF, &ru);
+  const double proc_ms = (ru.ru_utime.tv_sec + ru.ru_stime.tv_sec) * 1e3 + (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec) / 1e3;
+  std::vector<std::pair<std::string, double>> out;
+  double sum = main_ms;
+  for (int i = 0; i < kThrRoles; ++i) {
+    out.emplace_back(kThreadRoleNames[i] + 4, roles[i]);
+    sum += roles[i];
+  }
+  out.emplace_back("main", main_ms);
+  out.emplace_back("other_threads_live", other_live);
+  out.emplace_back("process", proc_ms);
+  out.emplace_back("unattributed", proc_ms - sum);
+  return out;
+}
 
 static std::mutex g_log_mu;
 

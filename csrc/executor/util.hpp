@@ -40,6 +40,24 @@ struct CpuScope {
   ~CpuScope() { g_cpu_ns[part] += thread_cpu_ns() - t0; }
 };
 
+// Whole-thread CPU by role (the CpuScopes above cover request handling only):
+// each daemon thread names itself and, when it exits, adds its CPU time to
+// its role; live threads are read from /proc/self/task at report time.  The
+// process total minus these is what threads we did not start cost (the HIP
+// runtime's, in a daemon with a kernel broker).
+enum ThreadRole { kThrHttp = 0, kThrWorkerReader, kThrZygoteReader, kThrBrokerPool, kThrAcceptor, kThrCleanup,
+                  kThrWatchdog, kThrRoles };
+extern std::atomic<int64_t> g_thread_exit_ns[kThrRoles];
+extern const char* const kThreadRoleNames[kThrRoles];
+struct ThreadRoleScope {
+  ThreadRole role;
+  explicit ThreadRoleScope(ThreadRole r);
+  ~ThreadRoleScope() { g_thread_exit_ns[role] += thread_cpu_ns(); }
+};
+// {role: ms} (exited + live threads), "process" (all threads, getrusage) and
+// "unattributed" (process - roles - the main thread)
+std::vector<std::pair<std::string, double>> thread_cpu_report();
+
 // ---- ids ------------------------------------------------------------------
 std::string random_hex(size_t nbytes);  // getrandom(2)-backed
 
