@@ -170,7 +170,6 @@ class SandboxPool {
   bool any_zygote_alive() const;
   // workers
   void worker_acceptor();
-  void worker_reader(int fd, pid_t peer);
   std::shared_ptr<Worker> spawn_worker(bool pooled, int kind, const std::string& gpus, const Json& extra_env,
                                        const std::string& fixed_ws = "", const std::string& fixed_rp = "",
                                        uid_t fixed_uid = 0, bool gang_rank = false);
@@ -235,6 +234,7 @@ class SandboxPool {
   std::atomic<uint64_t> rr_{0};
   std::atomic<bool> stopping_{false};
   int worker_listen_fd_ = -1;
+  int wake_fd_ = -1;  // eventfd: a zygote reported a pid (parked hellos re-check)
   std::string worker_sock_path_;
   std::thread acceptor_thread_, cleanup_thread_, watchdog_thread_;
   std::mutex cleanup_mu_;
