@@ -4,9 +4,11 @@
 #include <errno.h>
 #include <hip/hip_runtime_api.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
+#include <sys/prctl.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/un.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <cstring>
@@ -73,7 +75,31 @@ class HipDevice final : public broker::Device {
     // frees waiting for the stream work recorded before them (event, buffer)
     std::vector<std::pair<hipEvent_t, void*>> pending;
     std::vector<hipEvent_t> spare_events;
+    hipEvent_t wait_ev = nullptr;
   };
+
+  // Wait for everything queued on the session's stream with the thread
+  // asleep between checks.  HIP's own waits spin the calling core for the
+  // whole wait even under hipDeviceScheduleBlockingSync (measured on MI355X,
+  // tools/probe/sync_cpu_probe.hip: a 150 us kernel cost 159 us of CPU in
+  // hipStreamSynchronize, 7 us this way), and every reduce / read of every
+  // sandbox waits.  Checks 5 us apart at first, then every 20 us (the broker
+  // threads run with a 1 us timer slack).  BEE_BROKER_WAIT=spin: HIP's wait.
+  bool wait(Ctx* c) {
+    if (spin_wait_) return hipStreamSynchronize(c->s) == hipSuccess;
+    if (!c->wait_ev && hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming) != hipSuccess)
+      return hipStreamSynchronize(c->s) == hipSuccess;
+    if (hipEventRecord(c->wait_ev, c->s) != hipSuccess) return false;
+    long ns = 5000;
+    for (;;) {
+      const hipError_t e = hipEventQuery(c->wait_ev);
+      if (e == hipSuccess) return true;
+      if (e != hipErrorNotReady) return false;
+      timespec ts{0, ns};
+      nanosleep(&ts, nullptr);
+      if (ns < 20000) ns += 5000;
+    }
+  }
 
   // free the buffers whose recorded stream work has completed
   void reap(Ctx* c, bool all) {
@@ -199,15 +225,15 @@ class HipDevice final : public broker::Device {
   void free(void* p) override { bk.free_(p); }
   bool zero_async(void* p, uint64_t n, void* s) override { return hipMemsetAsync(p, 0, n, st(s)) == hipSuccess; }
   bool h2d_sync(void* d, const void* h, uint64_t n, void* s) override {
-    return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st(s)) == hipSuccess && hipStreamSynchronize(st(s)) == hipSuccess;
+    return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st(s)) == hipSuccess && wait((Ctx*)s);
   }
   bool d2h_sync(void* h, const void* d, uint64_t n, void* s) override {
-    return hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, st(s)) == hipSuccess && hipStreamSynchronize(st(s)) == hipSuccess;
+    return hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, st(s)) == hipSuccess && wait((Ctx*)s);
   }
   bool d2d_async(void* d, const void* src, uint64_t n, void* s) override {
     return hipMemcpyAsync(d, src, n, hipMemcpyDeviceToDevice, st(s)) == hipSuccess;
   }
-  bool sync(void* s) override { return hipStreamSynchronize(st(s)) == hipSuccess; }
+  bool sync(void* s) override { return wait((Ctx*)s); }
   int rand(uint32_t kind, void* y, int64_t n, uint32_t dt, uint64_t seed, uint64_t off, double a, double b,
            void* s) override {
     return kind == 0 ? bk.rand_uniform(y, n, (int)dt, seed, off, a, b, st(s)) : bk.rand_normal(y, n, (int)dt, seed, off, a, b, st(s));
@@ -228,12 +254,11 @@ class HipDevice final : public broker::Device {
   int fetch(Ctx* c, int rc, double* out) {
     if (rc != 0) return rc;
     if (c->slot == nullptr) {
-      if (hipMemcpyAsync(out, c->scalar, 8, hipMemcpyDeviceToHost, c->s) != hipSuccess ||
-          hipStreamSynchronize(c->s) != hipSuccess)
+      if (hipMemcpyAsync(out, c->scalar, 8, hipMemcpyDeviceToHost, c->s) != hipSuccess || !wait(c))
         return broker::kLaunchFailed;
       return 0;
     }
-    if (hipStreamSynchronize(c->s) != hipSuccess) return broker::kLaunchFailed;
+    if (!wait(c)) return broker::kLaunchFailed;
     *out = *(volatile double*)c->slot;
     return 0;
   }
@@ -274,6 +299,7 @@ class HipDevice final : public broker::Device {
   std::string arch() override { return arch_; }
 
  private:
+  bool spin_wait_ = getenv("BEE_BROKER_WAIT") && !strcmp(getenv("BEE_BROKER_WAIT"), "spin");
   void* lib_ = nullptr;
   std::string arch_;
   int64_t cus_ = 0, clock_ = 0, lds_ = 0;
@@ -357,6 +383,7 @@ void KernelBroker::accept_loop() {
 
 void KernelBroker::pool_thread() {
   ThreadRoleScope role(kThrBrokerPool);
+  prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // the GPU waits sleep in 5-20 us steps
   std::unique_lock<std::mutex> lk(q_mu_);
   while (!stopping_) {
     if (queue_.empty()) {

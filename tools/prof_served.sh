@@ -9,7 +9,13 @@ D=$(mktemp -d /tmp/bee-prof-XXXXXX)
 mkdir -p gpurun_out
 mapfile -t CMD < <(python tools/prof_served.py cmd "$D")
 export BEE_PROFILE_DAEMON_ONLY=1 TMPDIR=/tmp
-timeout -k 10 150 rocprofv3 --kernel-trace --marker-trace --stats -d gpurun_out/prof_served -o run -- "${CMD[@]}" \
+# PROF_FLAGS: what to trace (default kernels + the broker's roctx ranges;
+# e.g. "--hip-runtime-trace --marker-trace" for host time per HIP call);
+# PROF_DIR: output directory under gpurun_out
+FLAGS=${PROF_FLAGS:---kernel-trace --marker-trace --stats}
+OUT=${PROF_DIR:-gpurun_out/prof_served}
+# shellcheck disable=SC2086
+timeout -k 10 150 rocprofv3 $FLAGS -d "$OUT" -o run -- "${CMD[@]}" \
   > gpurun_out/prof_served_daemon.log 2>&1 &
 ROC=$!
 timeout -k 10 180 python tools/prof_served.py drive "$D" --n "$N"

@@ -1,7 +1,8 @@
 """Summarise a rocprofv3 SQLite output (rocpd schema) into small CSVs for
 profiles/: per-kernel call count / mean / min duration, and per-kernel mean
 PMC counter values when counters were collected, and per-range call count /
-mean duration of roctx ranges when markers were traced (--marker-trace).
+mean duration of roctx ranges when markers were traced (--marker-trace), and per-call
+host time of runtime API calls when traced (--hip-runtime-trace).
 
     python tools/rocpd_summary.py gpurun_out/prof/xxx_results.db profiles/name
 """
@@ -53,7 +54,20 @@ def main():
             w.writerow(["range", "calls", "mean_us", "min_us", "total_ms"])
             for m, n, avg, mn, tot in rg:
                 w.writerow([m, n, round(avg / 1e3, 2), round(mn / 1e3, 2), round(tot / 1e6, 2)])
-    print(f"{len(rows)} kernels, {len(pm)} counter rows, {len(rg)} ranges -> {prefix}_*.csv")
+    # runtime API calls (--hip-runtime-trace / --hsa-*-trace): host time per call
+    try:
+        api = list(cur.execute(
+            "select category, name, count(*), avg(end - start), sum(end - start) from regions "
+            "where category not like 'MARKER%' group by category, name order by sum(end - start) desc"))
+    except sqlite3.Error:
+        api = []
+    if api:
+        with open(prefix + "_api.csv", "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["category", "api", "calls", "mean_us", "total_ms"])
+            for cat, name, n, avg, tot in api:
+                w.writerow([cat, name, n, round(avg / 1e3, 2), round(tot / 1e6, 2)])
+    print(f"{len(rows)} kernels, {len(pm)} counter rows, {len(rg)} ranges, {len(api)} api rows -> {prefix}_*.csv")
 
 
 if __name__ == "__main__":
