@@ -83,21 +83,22 @@ class HipDevice final : public broker::Device {
   // whole wait even under hipDeviceScheduleBlockingSync (measured on MI355X,
   // tools/probe/sync_cpu_probe.hip: a 150 us kernel cost 159 us of CPU in
   // hipStreamSynchronize, 7 us this way), and every reduce / read of every
-  // sandbox waits.  Checks 5 us apart at first, then every 20 us (the broker
-  // threads run with a 1 us timer slack).  BEE_BROKER_WAIT=spin: HIP's wait.
+  // sandbox waits.  Checks 2 us apart at first, then every 10 us (the broker
+  // threads run with a 1 us timer slack): a request waits ~3 times, so the
+  // step bounds the latency it adds.  BEE_BROKER_WAIT=spin: HIP's wait.
   bool wait(Ctx* c) {
     if (spin_wait_) return hipStreamSynchronize(c->s) == hipSuccess;
     if (!c->wait_ev && hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming) != hipSuccess)
       return hipStreamSynchronize(c->s) == hipSuccess;
     if (hipEventRecord(c->wait_ev, c->s) != hipSuccess) return false;
-    long ns = 5000;
+    long ns = 2000;
     for (;;) {
       const hipError_t e = hipEventQuery(c->wait_ev);
       if (e == hipSuccess) return true;
       if (e != hipErrorNotReady) return false;
       timespec ts{0, ns};
       nanosleep(&ts, nullptr);
-      if (ns < 20000) ns += 5000;
+      if (ns < 10000) ns += 2000;
     }
   }
 
