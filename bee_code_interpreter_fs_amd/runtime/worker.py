@@ -68,6 +68,7 @@ def _json_str(s: str) -> str:
 
 
 _OUT_FDS: dict = {}  # stdout / stderr / timing.json, opened before the jail
+_REDIRECTED: list = []  # [stdout path, stderr path] once fds 1 / 2 point at the run's files
 
 
 def _open_outputs(meta_dir: str) -> None:
@@ -84,6 +85,7 @@ def _redirect_stdio(stdout_path: str, stderr_path: str) -> None:
     flags = os.O_WRONLY | os.O_CREAT | os.O_TRUNC
     out_fd = _OUT_FDS.pop("stdout", None)
     err_fd = _OUT_FDS.pop("stderr", None)
+    _REDIRECTED[:] = [stdout_path, stderr_path]
     if out_fd is None:
         out_fd = os.open(stdout_path, flags, 0o600)
     if err_fd is None:
@@ -222,17 +224,29 @@ def _run_main(path: str) -> None:
 _KEEP: list = []
 
 
-def run_script(script: str, argv, workspace: str, runtime_packages: str) -> int:
-    sys.argv = [script, *argv]
-    script_dir = os.path.dirname(os.path.abspath(script))
+_PATHS_FOR: list = []  # the runtime-packages view _prepare_paths ran for
+
+
+def _prepare_paths(runtime_packages: str) -> None:
+    """sys.path and PYTHONPATH of a `python script.py` run with the
+    runtime-packages tree importable (what the reference's image set up);
+    done while pooled, the script's own directory is added at run time."""
     sys.path[:] = [p for p in sys.path if p not in ("", ".")]
-    sys.path.insert(0, script_dir)
     if runtime_packages and runtime_packages not in sys.path:
-        sys.path.insert(1, runtime_packages)
+        sys.path.insert(0, runtime_packages)
     if SANDBOX_SITE not in sys.path:
         sys.path.append(SANDBOX_SITE)
     pp = os.environ.get("PYTHONPATH", "")
     os.environ["PYTHONPATH"] = os.pathsep.join(p for p in (runtime_packages, SANDBOX_SITE, pp) if p)
+    _PATHS_FOR[:] = [runtime_packages]
+
+
+def run_script(script: str, argv, workspace: str, runtime_packages: str) -> int:
+    sys.argv = [script, *argv]
+    script_dir = os.path.dirname(os.path.abspath(script))
+    if _PATHS_FOR != [runtime_packages]:
+        _prepare_paths(runtime_packages)
+    sys.path.insert(0, script_dir)
     from . import sandbox_patches
 
     sandbox_patches.install()
@@ -494,6 +508,15 @@ def _serve(cwd: str, chan: _Chan) -> None:
             _prefault()
         _prefault_scientific()
         _cpu_stamp("prefault")
+        # what the run needs that does not depend on the request, done while
+        # pooled: stdout / stderr onto the run's files (opened at boot) and
+        # the /workspace view -- the request path then starts the script
+        meta = os.environ.get("BEE_META_DIR", "")
+        if meta and "stdout" in _OUT_FDS and "stderr" in _OUT_FDS:
+            _redirect_stdio(os.path.join(meta, "stdout"), os.path.join(meta, "stderr"))
+        rp = os.environ.get("BEE_RUNTIME_PACKAGES", "")
+        ws_view, rp_view = _logical_view(cwd, rp)
+        _prepare_paths(rp_view)
         chan.send(('{"op":"ready","warm_ms":%.3f,"gpu_error":%s}\n'
                    % ((time.perf_counter() - t0) * 1e3, _json_str(gpu_error or ""))).encode())
         job = chan.recv_json()
@@ -503,19 +526,22 @@ def _serve(cwd: str, chan: _Chan) -> None:
         ru = resource.getrusage(resource.RUSAGE_SELF)  # CPU spent while pooled (warm-up, prefault)
         _STAMPS["cpu_pool_ms"] = (ru.ru_utime + ru.ru_stime) * 1e3
         _STAMPS["minflt_pool"] = ru.ru_minflt
-        for k, v in (job.get("env") or {}).items():
+        job_env = job.get("env") or {}
+        for k, v in job_env.items():
             os.environ[k] = str(v)
         _apply_job_quota(int(job.get("hbm_quota") or 0))
-        _redirect_stdio(job["stdout"], job["stderr"])
+        if _REDIRECTED != [job["stdout"], job["stderr"]]:
+            _redirect_stdio(job["stdout"], job["stderr"])
         _STAMPS["redir"] = time.monotonic() * 1e3
     except BaseException:
         try:
             traceback.print_exc()
         finally:
             os._exit(70)
-    rp = os.environ.get("BEE_RUNTIME_PACKAGES", "")
     script = job["script"]
-    ws_view, rp_view = _logical_view(cwd, rp)
+    if "TMPDIR" in job_env or "BEE_RUNTIME_PACKAGES" in job_env:  # the request moved what the view maps
+        rp = os.environ.get("BEE_RUNTIME_PACKAGES", "")
+        ws_view, rp_view = _logical_view(cwd, rp)
     _STAMPS["view"] = time.monotonic() * 1e3
     if ws_view != cwd:
         script = _to_logical(script, cwd, ws_view)
