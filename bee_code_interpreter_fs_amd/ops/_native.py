@@ -111,6 +111,11 @@ def _declare(lib: ctypes.CDLL) -> None:
             c_int,
         ),
         "bk_gemm_bf16_pick": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int], c_int),
+        "bk_gemm_bf16_nn": (
+            [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_f, c_int, c_vp],
+            c_int,
+        ),
+        "bk_gemm_bf16_nn_ok": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int], c_int),
         "bk_transpose_bf16": ([c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),
         "bk_transpose_to_bf16": ([c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),
         "bk_transpose": ([c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),

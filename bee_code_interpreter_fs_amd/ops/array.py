@@ -537,13 +537,22 @@ def power(a, b): return _binary("power", a, b)
 
 # ---- matmul --------------------------------------------------------------------------
 
+# The [K][N] kernel (bk_gemm_bf16_nn) is correct but not yet faster than
+# transpose + TN: the compiler puts an s_waitcnt vmcnt(0) before every
+# ds_read_b64_tr_b16 (the intrinsic's memory operand defeats the LDS-DMA alias
+# check), serialising its B reads behind the in-flight tile loads -- 595 vs
+# 1193 TFLOP/s at 4096^3 (profiles/r2_gemm_nn_bench.log).  Opt-in until then.
+_GEMM_NN = os.environ.get("BEE_GEMM_NN", "0") == "1"
+
+
 def matmul(a, b, out_dtype: str = "bfloat16") -> DeviceArray:
     """C = A @ B on the bf16 MFMA GEMM (f32 accumulate).
 
-    ``b`` is consumed as Bt[N, K] (K-contiguous): ``b.T`` views of a
-    row-major [N, K] buffer are used as is; a plain row-major ``b`` is
-    transposed once on device (15 us at 4096^2, ~12 % of a 4096^3 GEMM); an
-    f32/f64 ``b`` is converted and transposed in the same pass.
+    ``b.T`` views of a row-major [N, K] buffer are used as is (the TN
+    kernels); a plain row-major ``b`` is transposed once on device (15 us at
+    4096^2) -- or, with BEE_GEMM_NN=1, read in place by the [K][N] kernel for
+    tile-multiple shapes; an f32/f64 ``b`` is converted and transposed in the
+    same pass.
     """
     a = _as_operand(a)
     b = _as_operand(b)
@@ -572,6 +581,16 @@ def matmul(a, b, out_dtype: str = "bfloat16") -> DeviceArray:
         if b.dtype != "bfloat16":
             b = b.astype("bfloat16")
         b._materialize()
+        out_dtype = normalize_dtype(out_dtype)
+        from .driver import nn_shape_ok
+
+        d = driver()
+        if _GEMM_NN and hasattr(d, "gemm_nn") and nn_shape_ok(M, N, K, K, N, N, out_dtype == "bfloat16") and \
+                (d.name == "broker" or (a.ptr % 16 == 0 and b.ptr % 16 == 0)):
+            # B[K, N] read in place through transposed LDS reads: no transpose pass
+            c = DeviceArray((M, N), out_dtype)
+            d.gemm_nn(a.ptr, b.ptr, c.ptr, M, N, K, K, N, N, 1.0, 0.0, DTYPE_CODES[out_dtype])
+            return c
         keep = DeviceArray((N, K), "bfloat16")
         driver().transpose(b.ptr, keep.ptr, K, N, N, K)
         bt_ptr = keep.ptr

@@ -100,6 +100,13 @@ class NativeDriver:
             "bk_gemm_bf16_tn",
         )
 
+    def gemm_nn(self, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, odt) -> None:
+        """C = A . B with B stored [K][N] (callers check nn_shape_ok first)."""
+        check(
+            self.lib.bk_gemm_bf16_nn(_vp(A), _vp(B), _vp(C), M, N, K, lda, ldb, ldc, alpha, beta, odt, self.stream),
+            "bk_gemm_bf16_nn",
+        )
+
     def reduce_axis(self, op: int, dt: int, x: int, y: int, rows: int, cols: int, ld: int, axis: int) -> None:
         if not self.axis_ws:
             self.axis_ws = self.malloc(self.lib.bk_reduce_axis_workspace_bytes())
@@ -371,6 +378,10 @@ class BrokerDriver:
     def gemm(self, A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt) -> None:
         self._post(GEMM, struct.pack("<QQQiiiiiiffii", A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, 0))
 
+    def gemm_nn(self, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, odt) -> None:
+        # flags bit 0: the second operand is B[K][N] (broker_core.cpp kGemmNN)
+        self._post(GEMM, struct.pack("<QQQiiiiiiffii", A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, 1))
+
     def reduce_axis(self, op, dt, x, y, rows, cols, ld, axis) -> None:
         self._post(REDUCE_AXIS, struct.pack("<IIQQqqqII", op, dt, x, y, rows, cols, ld, axis, 0))
 
@@ -409,6 +420,16 @@ class BrokerDriver:
     def timer_stop(self, tok) -> float:
         self.sync()
         return (time.perf_counter() - tok) * 1e3
+
+
+def nn_shape_ok(M: int, N: int, K: int, lda: int, ldb: int, ldc: int, out_bf16: bool) -> bool:
+    """Shapes the [K][N]-B GEMM kernel takes (gemm256w4_impl.hpp nn_ok), and
+    large enough to fill the chip with 256^2 tiles (smaller ones go to the
+    128^2 kernel after a transpose).  Pointers must be 16-B aligned too."""
+    span = lambda ld: 256 * ld * 2 + K * 2 < 0x7FFFFFFF  # noqa: E731
+    return (M > 0 and N > 0 and K > 0 and M % 256 == 0 and N % 256 == 0 and K % 64 == 0 and lda % 8 == 0
+            and ldb % 8 == 0 and ldb >= N and ldc % (8 if out_bf16 else 4) == 0 and span(lda)
+            and K * ldb * 2 < 0x7FFFFFFF and (M // 256) * (N // 256) >= 128)
 
 
 def make_driver():

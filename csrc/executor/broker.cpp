@@ -56,6 +56,7 @@ class HipDevice final : public broker::Device {
     int (*rand_reduce)(int, int, int64_t, uint64_t, uint64_t, double, double, void*, void*, hipStream_t);
     int (*reduce)(int, int, const void*, const void*, int64_t, void*, void*, hipStream_t);
     int (*gemm)(const void*, const void*, void*, int, int, int, int, int, int, float, float, int, hipStream_t);
+    int (*gemm_nn)(const void*, const void*, void*, int, int, int, int, int, int, float, float, int, hipStream_t);
     int (*transpose)(int, int, const void*, void*, int, int, int, int, hipStream_t);
     int (*preload)(hipStream_t);
     int64_t (*axis_ws)();
@@ -138,6 +139,7 @@ class HipDevice final : public broker::Device {
     sym(lib_, "bk_preload", &bk.preload);
     sym(lib_, "bk_reduce_axis_workspace_bytes", &bk.axis_ws);
     sym(lib_, "bk_reduce_axis", &bk.reduce_axis);
+    sym(lib_, "bk_gemm_bf16_nn", &bk.gemm_nn);
     return true;
   }
 
@@ -276,6 +278,11 @@ class HipDevice final : public broker::Device {
   int gemm(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
            float beta, int odt, void* s) override {
     return bk.gemm(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, st(s));
+  }
+  int gemm_nn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
+              float beta, int odt, void* s) override {
+    if (!bk.gemm_nn) return broker::kBadArgument;
+    return bk.gemm_nn(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, st(s));
   }
   int transpose(int sdt, int ddt, const void* in, void* out, int rows, int cols, int ldi, int ldo, void* s) override {
     return bk.transpose(sdt, ddt, in, out, rows, cols, ldi, ldo, st(s));

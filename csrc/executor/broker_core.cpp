@@ -324,15 +324,19 @@ int32_t Session::dispatch(uint32_t op, const char* payload, uint64_t len, std::v
       const int32_t lda = r.get<int32_t>(), ldb = r.get<int32_t>(), ldc = r.get<int32_t>();
       const float alpha = r.get<float>(), beta = r.get<float>();
       const int32_t odt = r.get<int32_t>();
+      const uint32_t gflags = r.get<uint32_t>();  // kGemmNN: the second operand is B[K][N], not Bt[N][K]
       if (!r.ok) return kProtocol;
+      const bool nn = (gflags & kGemmNN) != 0;
       uint64_t na, nb, nc;
       Buf *ba = lookup(A), *bb = lookup(Bt), *bc = lookup(C);
-      if ((odt != 0 && odt != 2) || !matrix_bytes(M, K, lda, 2, &na) || !matrix_bytes(N, K, ldb, 2, &nb) ||
+      if ((odt != 0 && odt != 2) || (gflags & ~kGemmNN) != 0 || !matrix_bytes(M, K, lda, 2, &na) ||
+          !(nn ? matrix_bytes(K, N, ldb, 2, &nb) : matrix_bytes(N, K, ldb, 2, &nb)) ||
           !matrix_bytes(M, N, ldc, dtype_size((uint32_t)odt), &nc) || !ba || !bb || !bc || na > ba->size ||
           nb > bb->size || nc > bc->size)
         return kBadHandle;
       const bool c_full = beta == 0.f && ldc == N;  // every byte of C[0:M*N] written, nothing read
       if (!will_read(ba) || !will_read(bb) || !(c_full ? will_write(bc, 0, nc) : will_read(bc))) return kLaunchFailed;
+      if (nn) return dev_.gemm_nn(ba->ptr, bb->ptr, bc->ptr, M, N, K, lda, ldb, ldc, alpha, beta, odt, stream_);
       return dev_.gemm(ba->ptr, bb->ptr, bc->ptr, M, N, K, lda, ldb, ldc, alpha, beta, odt, stream_);
     }
     case kTranspose: {

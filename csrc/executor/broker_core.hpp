@@ -33,6 +33,7 @@ enum Status : int32_t {
   kBadHandle = 6, kProtocol = 7,
 };
 constexpr uint32_t kNoReply = 1;                   // request flag
+constexpr uint32_t kGemmNN = 1;                    // GEMM payload flags: B stored [K][N]
 constexpr uint64_t kMaxFrame = 1ull << 30;         // largest request / READ reply
 constexpr int64_t kMaxLazyDraw = 1ll << 36;        // rand_reduce: ~70 ms of GPU at most
 constexpr uint64_t kMaxClientHandle = 1ull << 62;  // ALLOC_AT ids are 1 .. 2^62-1
@@ -84,6 +85,11 @@ class Device {
                           double* out, void* s) = 0;
   virtual int gemm(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
                    float beta, int odt, void* s) = 0;
+  // C = A . B with B stored [K][N]; kBadArgument where the device has no such
+  // kernel for the shape (the client then transposes and uses gemm)
+  virtual int gemm_nn(const void*, const void*, void*, int, int, int, int, int, int, float, float, int, void*) {
+    return kBadArgument;
+  }
   virtual int transpose(int sdt, int ddt, const void* in, void* out, int rows, int cols, int ldi, int ldo, void* s) = 0;
   // per-column (axis 0) / per-row (axis 1) sum or mean into y (f64 for f64 x, else f32)
   virtual int reduce_axis(uint32_t op, uint32_t dt, const void* x, void* y, int64_t rows, int64_t cols, int64_t ld,

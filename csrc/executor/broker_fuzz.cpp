@@ -118,6 +118,18 @@ class HostDevice final : public Device {
     }
     return 0;
   }
+  int gemm_nn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, float, float beta,
+              int odt, void*) override {
+    for (int i = 0; i < M; ++i) sum((const char*)A + (uint64_t)i * lda * 2, (uint64_t)K * 2);
+    for (int k = 0; k < K; ++k) sum((const char*)B + (uint64_t)k * ldb * 2, (uint64_t)N * 2);
+    const uint64_t es = odt == 0 ? 4 : 2;
+    for (int i = 0; i < M; ++i) {
+      char* row = (char*)C + (uint64_t)i * ldc * es;
+      if (beta != 0.f) sum(row, (uint64_t)N * es);
+      touch_w(row, (uint64_t)N * es, 0);
+    }
+    return 0;
+  }
   int transpose(int sdt, int ddt, const void* in, void* out, int rows, int cols, int ldi, int ldo, void*) override {
     const uint64_t si = dtype_size((uint32_t)sdt), so = dtype_size((uint32_t)ddt);
     for (int i = 0; i < rows; ++i) sum((const char*)in + (uint64_t)i * ldi * si, (uint64_t)cols * si);

@@ -86,6 +86,9 @@ enum : int {
   // block when ldc breaks the vector stores' alignment -- store element by
   // element under a mask
   kEdge = 1024,
+  // B given as [K][N] (C = A . B): transposed LDS reads, see make_panel_nn
+  // (tile-multiple shapes, K % 64 == 0)
+  kNN = 2048,
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
@@ -109,7 +112,8 @@ __device__ __forceinline__ void barrier() {
 // 64-bit per-lane pointers, and rows past the panel read as zero.
 struct Panel {
   __amdgpu_buffer_rsrc_t rsrc;
-  int lane_off[2];  // bytes: (lane/8) rows + this lane's swizzled 16-B chunk, for even / odd i
+  int lane_off[4];  // bytes: (lane/8) rows + this lane's swizzled 16-B chunk, for even / odd i
+                    // (kNN B panels: 4 variants, see make_panel_nn)
   int row_bytes;    // ld * 2
   int k_lim[2];     // kEdge: this lane's chunk holds K columns while k0 < k_lim (K - 8 * chunk)
 };
@@ -138,6 +142,65 @@ __device__ __forceinline__ Panel make_panel(const uint16_t* base, int ld, int la
   return p;
 }
 
+// ---- kNN: B stored [K][N] (row-major, ldb >= N) ------------------------------
+// The B K-tile is staged as its own 64 rows (k) x 256 columns (n) of 512 B,
+// 32-B units XOR-swizzled by f(row) = (row & 3) | ((row >> 3) & 1) << 2, and
+// each MFMA B fragment (8 consecutive k of one n per lane) is read with two
+// ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group, delivered
+// column-major: cdna_hip_programming.md T10).  Within a 32-lane half the two
+// groups read rows 8 apart; f maps the 8 rows to 8 distinct 32-B bank
+// windows, so the transposed reads are conflict-free.  glds writes LDS
+// lane-linearly, so each lane fetches the global chunk that belongs at its
+// LDS slot (the inverse swizzle in its offset).
+__device__ __forceinline__ int nn_f(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
+
+__device__ __forceinline__ Panel make_panel_nn(const uint16_t* base, int ld, int lane, int K) {
+  Panel p;
+  const uint64_t addr = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)addr);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(addr >> 32));
+  const int64_t span = (int64_t)K * ld * 2;
+  const uint32_t bytes = __builtin_amdgcn_readfirstlane(span > 0xffffffffll ? 0xffffffffu : (uint32_t)span);
+  p.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+  p.row_bytes = ld * 2;
+  const int b = lane >> 5, pos16 = lane & 31;
+  // glds instruction i of a wave fills LDS rows 2*(8*wave + i) + b; f of
+  // that row depends on i only through (i & 1) and (i >> 2)
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int i = (v & 1) | ((v >> 1) << 2);
+    const int f = ((2 * i + b) & 3) | ((i >> 2) << 2);
+    const int u = (pos16 >> 1) ^ f;
+    p.lane_off[v] = b * ld * 2 + (u * 2 + (pos16 & 1)) * 16;
+  }
+  p.k_lim[0] = p.k_lim[1] = 0;
+  return p;
+}
+
+__device__ __forceinline__ void glds_nn(const Panel& p, int k0, uint16_t* lds_operand, int wave, int i) {
+  const int soff = (k0 + (wave * 8 + i) * 2) * p.row_bytes;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(p.rsrc, (lds_void_ptr)(lds_operand + (wave * kGlds + i) * 8 * TK), 16,
+                                           p.lane_off[(i & 1) | ((i >> 2) << 1)], soff, 0, 0);
+}
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// B fragment of n-block u (16 columns: u in 0..15 of the 256) for k-half s
+__device__ __forceinline__ bf16x8 frag_nn(const uint16_t* lds_b, int u, int s, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  s16x4 v[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = s * 32 + 8 * g + 4 * h + q;
+    const uint16_t* a = lds_b + row * 256 + ((u ^ nn_f(row)) * 16) + p * 4;
+    v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const_cast<uint16_t*>(a)));
+  }
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  const s16x8 w = {v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3]};
+  return __builtin_bit_cast(bf16x8, w);
+}
+
 // a lane's 16-B chunk at column k0 + 8 * chunk: past K (the ragged last
 // K-tile of kEdge) its offset becomes 2^31, beyond every panel's extent, and
 // the load returns zeros.  (K % 8 == 0: chunks are all in or all out.)
@@ -149,7 +212,13 @@ __device__ __forceinline__ int chunk_off(const Panel& p, int k0, int par, bool k
 
 // stage one operand's K-tile: 8 wave-instructions of 1 KiB (8 rows) each;
 // `wave` must be wave-uniform (readfirstlane'd) so the LDS base goes to M0
-__device__ __forceinline__ void stage(const Panel& p, int k0, uint16_t* lds_operand, int wave, bool kt = false) {
+__device__ __forceinline__ void stage(const Panel& p, int k0, uint16_t* lds_operand, int wave, bool kt = false,
+                                      bool nn = false) {
+  if (nn) {
+#pragma unroll
+    for (int i = 0; i < kGlds; ++i) glds_nn(p, k0, lds_operand, wave, i);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < kGlds; ++i) {
     const int soff = (wave * 64 + i * 8) * p.row_bytes + k0 * 2;
@@ -162,13 +231,19 @@ __device__ __forceinline__ bf16x8 frag(const uint16_t* lds_operand, int row, int
   return *reinterpret_cast<const bf16x8*>(lds_operand + row * TK + swz(row, chunk) * 8);
 }
 
+// B fragment j (columns wc*128 + j*16 ...) of k-half s, either layout
+__device__ __forceinline__ bf16x8 fragB(const uint16_t* lds_b, int wc, int j, int s, int lane, bool nn) {
+  if (nn) return frag_nn(lds_b, wc * 8 + j, s, lane);
+  return frag(lds_b, wc * 128 + j * 16 + (lane & 15), s * 4 + (lane >> 4));
+}
+
 // the 8 A (rows wr*128 + i*16 + lane&15) and 8 B fragments of k-half s
 __device__ __forceinline__ void read_frags(const uint16_t* buf, int wr, int wc, int lane, int s, bf16x8 (&fa)[8],
-                                           bf16x8 (&fb)[8]) {
+                                           bf16x8 (&fb)[8], bool nn = false) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) fa[i] = frag(buf, wr * 128 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
 #pragma unroll
-  for (int j = 0; j < 8; ++j) fb[j] = frag(buf + kOperand, wc * 128 + j * 16 + (lane & 15), s * 4 + (lane >> 4));
+  for (int j = 0; j < 8; ++j) fb[j] = fragB(buf + kOperand, wc, j, s, lane, nn);
 }
 
 template <bool ASM = false>
@@ -230,7 +305,7 @@ __device__ __forceinline__ void glds_one(const Panel& p, int k0, uint16_t* lds_o
 // A ds_read overwrites a fragment register >= 16 MFMAs after its last reader
 // (WAR on srcA/B of an in-flight MFMA, invisible to the hazard recognizer
 // through inline asm).
-template <bool INIT, bool EARLY, bool READS_EARLY, bool KT = false>
+template <bool INIT, bool EARLY, bool READS_EARLY, bool KT = false, bool NN = false>
 __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8], bf16x8 (&fa1)[8],
                                           bf16x8 (&fb1)[8], uint16_t* smem, const Panel& pa, const Panel& pb, int t,
                                           int nk, int wr, int wc, int lane, int wave) {
@@ -244,7 +319,7 @@ __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], 
     for (int jj = 0; jj < 4; ++jj) mfma_asm<INIT>(acc[g >> 1][(g & 1) * 4 + jj], fa0[g >> 1], fb0[(g & 1) * 4 + jj]);
     auto read1 = [&](int i) {  // i-th of the 16 k-half-1 fragments: fa1[0..7], fb1[0..7]
       if (i < 8) fa1[i] = frag(cur, wr * 128 + i * 16 + rl, 4 + ch);
-      else fb1[i - 8] = frag(cur + kOperand, wc * 128 + (i - 8) * 16 + rl, 4 + ch);
+      else fb1[i - 8] = fragB(cur + kOperand, wc, i - 8, 1, lane, NN);
     };
     if constexpr (READS_EARLY) {
       // all 16 reads by group 11 (2 per group in 0..3): the lgkmcnt(0) before
@@ -270,16 +345,18 @@ __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], 
     if constexpr (EARLY) {  // all 16 glds in the first 8 groups: more time to land
       if (g < 8) {
         glds_one(pa, kn, cur, wave, g, KT);
-        glds_one(pb, kn, cur + kOperand, wave, g, KT);
+        if constexpr (NN) glds_nn(pb, kn, cur + kOperand, wave, g);
+        else glds_one(pb, kn, cur + kOperand, wave, g, KT);
       }
     } else {
       if (g < 8) glds_one(pa, kn, cur, wave, g, KT);
+      else if constexpr (NN) glds_nn(pb, kn, cur + kOperand, wave, g - 8);
       else glds_one(pb, kn, cur + kOperand, wave, g - 8, KT);
     }
     // in the order the next K-tile's first groups consume them: fa0[0],
     // fb0[0..7], fa0[1..7]
     if (g == 0) fa0[0] = frag(nxt, wr * 128 + rl, ch);
-    else if (g <= 8) fb0[g - 1] = frag(nxt + kOperand, wc * 128 + (g - 1) * 16 + rl, ch);
+    else if (g <= 8) fb0[g - 1] = fragB(nxt + kOperand, wc, g - 1, 0, lane, NN);
     else fa0[g - 8] = frag(nxt, wr * 128 + (g - 8) * 16 + rl, ch);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -389,7 +466,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   constexpr bool pin = (O & kPinOrder) != 0, inter = (O & kInterleave) != 0, am = (O & kAsmMfma) != 0,
                  early = (O & kEarlyGlds) != 0, reads_early = (O & kReadsEarly) != 0;
 
-  constexpr bool edge = (O & kEdge) != 0;
+  constexpr bool edge = (O & kEdge) != 0, nn = (O & kNN) != 0;
+  static_assert(!(edge && nn), "kNN is for tile-multiple shapes");
   const int nbm = edge ? (M + TM - 1) / TM : M / TM, nbn = edge ? (N + TN - 1) / TN : N / TN, nblocks = nbm * nbn;
   const int b = xcd_remap(blockIdx.x, nblocks);
   constexpr int kGm = (O & kGroup2) ? 2 : (O & kGroup8) ? 8 : (O & kGroup16) ? 16 : kGroupM;
@@ -403,7 +481,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 1, wc = wave & 1;
   const Panel pa = make_panel(A + (int64_t)m0 * lda, lda, lane, edge ? min(TM, M - m0) : TM, K);
-  const Panel pb = make_panel(Bt + (int64_t)n0 * ldb, ldb, lane, edge ? min(TN, N - n0) : TN, K);
+  const Panel pb = nn ? make_panel_nn(Bt + n0, ldb, lane, K)
+                      : make_panel(Bt + (int64_t)n0 * ldb, ldb, lane, edge ? min(TN, N - n0) : TN, K);
 
   f32x4 acc[8][8];
 #pragma unroll
@@ -414,10 +493,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   const int nk = edge ? (K + TK - 1) / TK : K / TK;  // kEdge: a ragged last K-tile reads zeros past K
   // prologue: tiles 0 and 1 in flight, wait for tile 0 (16 glds per tile)
   stage(pa, 0, smem, wave, edge);
-  stage(pb, 0, smem + kOperand, wave, edge);
+  stage(pb, 0, smem + kOperand, wave, edge, nn);
   if (nk > 1) {
     stage(pa, TK, smem + kBuf, wave, edge);
-    stage(pb, TK, smem + kBuf + kOperand, wave, edge);
+    stage(pb, TK, smem + kBuf + kOperand, wave, edge, nn);
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -428,31 +507,31 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   if constexpr (am && inter) {
     // hand-interleaved pipeline; K-tile 0 peeled so its MFMAs start the
     // accumulators from the constant 0 (no AGPR zero-fill to fence)
-    read_frags(smem, wr, wc, lane, 0, fa0, fb0);
-    ktile_asm<true, early, reads_early, edge>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
-    for (int t = 1; t < nk; ++t) ktile_asm<false, early, reads_early, edge>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
+    read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn);
+    ktile_asm<true, early, reads_early, edge, nn>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
+    for (int t = 1; t < nk; ++t) ktile_asm<false, early, reads_early, edge, nn>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
   } else if constexpr ((O & kNoCarry) != 0) {
     // loop-carried state is the accumulators only (simpler register
     // allocation); the first MFMAs of each K-tile wait for its first reads
     for (int t = 0; t < nk; ++t) {
       uint16_t* cur = smem + (t & 1) * kBuf;
-      read_frags(cur, wr, wc, lane, 0, fa0, fb0);
-      read_frags(cur, wr, wc, lane, 1, fa1, fb1);
+      read_frags(cur, wr, wc, lane, 0, fa0, fb0, nn);
+      read_frags(cur, wr, wc, lane, 1, fa1, fb1, nn);
       mfma_block<am>(acc, fa0, fb0);
       mfma_block<am>(acc, fa1, fb1);
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       barrier();
       const int kn = min(t + 2, nk - 1) * TK;
       stage(pa, kn, cur, wave, edge);
-      stage(pb, kn, cur + kOperand, wave, edge);
+      stage(pb, kn, cur + kOperand, wave, edge, nn);
     }
   } else {
-  read_frags(smem, wr, wc, lane, 0, fa0, fb0);
+  read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn);
   for (int t = 0; t < nk; ++t) {
     uint16_t* cur = smem + (t & 1) * kBuf;
     uint16_t* nxt = smem + ((t & 1) ^ 1) * kBuf;
 
-    read_frags(cur, wr, wc, lane, 1, fa1, fb1);
+    read_frags(cur, wr, wc, lane, 1, fa1, fb1, nn);
     if constexpr (inter) interleave_hint<16, 0>();
     else if constexpr (pin) __builtin_amdgcn_sched_barrier(0);
     mfma_block<am>(acc, fa0, fb0);
@@ -466,8 +545,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
     // and read fragments nobody uses
     const int kn = min(t + 2, nk - 1) * TK;
     stage(pa, kn, cur, wave, edge);
-    stage(pb, kn, cur + kOperand, wave, edge);
-    read_frags(nxt, wr, wc, lane, 0, fa0, fb0);
+    stage(pb, kn, cur + kOperand, wave, edge, nn);
+    read_frags(nxt, wr, wc, lane, 0, fa0, fb0, nn);
     if constexpr (inter) interleave_hint<16, 16>();
     else if constexpr (pin) __builtin_amdgcn_sched_barrier(0);
     mfma_block<am>(acc, fa1, fb1);
@@ -511,6 +590,13 @@ inline bool ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16) {
   const auto span_ok = [K](int ld) { return (int64_t)256 * ld * 2 + (int64_t)K * 2 < 0x7fffffffll; };
   return M > 0 && N > 0 && K > 0 && M % TM == 0 && N % TN == 0 && K % TK == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
          ldc % (out_bf16 ? 8 : 4) == 0 && span_ok(lda) && span_ok(ldb);
+}
+
+// kNN: B is [K][N]; tile multiples; the K x ldb panel within 31-bit offsets
+inline bool nn_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16) {
+  const auto span_ok = [K](int ld) { return (int64_t)256 * ld * 2 + (int64_t)K * 2 < 0x7fffffffll; };
+  return M > 0 && N > 0 && K > 0 && M % TM == 0 && N % TN == 0 && K % TK == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+         ldb >= N && ldc % (out_bf16 ? 8 : 4) == 0 && span_ok(lda) && (int64_t)K * ldb * 2 < 0x7fffffffll;
 }
 
 // kEdge: any M, N; the rest as ok()

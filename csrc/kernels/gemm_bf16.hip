@@ -542,6 +542,9 @@ bool gemm256_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16); 
 void launch_gemm256(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
                     float beta, bool out_bf16, hipStream_t stream, int which);
 bool gemm256_edge_ok(int M, int N, int K, int lda, int ldb);
+bool gemm256_nn_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16);
+void launch_gemm256_nn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                       float alpha, float beta, bool out_bf16, hipStream_t stream);
 void launch_gemm256_edge(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                          float alpha, float beta, bool out_bf16, hipStream_t stream);
 
@@ -665,6 +668,24 @@ BK_API int bk_gemm_bf16_pick(const void* A, const void* Bt, const void* C, int M
   const bool ok128 = al && bk_gemm_bf16_fast_ok(M, N, K, lda, ldb);
   const bool ok256 = al && aligned16(C) && gemm256_ok(M, N, K, lda, ldb, ldc, out_dtype == kBF16);
   return auto_variant(ok256, ok128, al && edge_ok(M, N, K, lda, ldb), al && gemm256_edge_ok(M, N, K, lda, ldb), M, N);
+}
+
+// C = alpha * A . B + beta * C with B stored [K][N] (leading dimension ldb):
+// the 4-wave 256x256 kernel reading B through transposed LDS reads, no
+// transpose pass.  Tile-multiple shapes (M, N % 256, K % 64) with 16-B
+// aligned operands only: kBadArgument otherwise (callers transpose B and use
+// bk_gemm_bf16_tn).
+BK_API int bk_gemm_bf16_nn_ok(const void* A, const void* B, const void* C, int M, int N, int K, int lda, int ldb,
+                              int ldc, int out_dtype) {
+  return A && B && C && (out_dtype == kBF16 || out_dtype == kF32) && lda >= K && ldc >= N && aligned16(A) &&
+         aligned16(B) && aligned16(C) && gemm256_nn_ok(M, N, K, lda, ldb, ldc, out_dtype == kBF16);
+}
+
+BK_API int bk_gemm_bf16_nn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                           float alpha, float beta, int out_dtype, hipStream_t stream) {
+  if (!bk_gemm_bf16_nn_ok(A, B, C, M, N, K, lda, ldb, ldc, out_dtype)) return kBadArgument;
+  launch_gemm256_nn(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, out_dtype == kBF16, stream);
+  return launch_status();
 }
 
 // C = alpha * A . Bt^T + beta * C.  out_dtype: kBF16 or kF32.

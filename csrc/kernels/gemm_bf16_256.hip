@@ -30,13 +30,4 @@ void launch_gemm256(const void* A, const void* Bt, void* C, int M, int N, int K,
     g256::launch<kShipped>(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, out_bf16, stream);
 }
 
-// the 4-wave 256x256 kernel on any M x N (K a multiple of 64): ragged
-// borders read zeros and store under a mask (g4::kEdge)
-bool gemm256_edge_ok(int M, int N, int K, int lda, int ldb) { return g4::edge_ok(M, N, K, lda, ldb); }
-
-void launch_gemm256_edge(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-                         float alpha, float beta, bool out_bf16, hipStream_t stream) {
-  g4::launch<kShippedW4 | g4::kEdge>(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, out_bf16, stream);
-}
-
 }  // namespace bk

@@ -192,7 +192,7 @@ def _random_frames(seed: int, n: int):
             payload = struct.pack("<IIQQQ", small(), small(), h(), h(), num())
         elif op == GEMM:
             payload = struct.pack("<QQQiiiiiiffii", h(), h(), h(), i32(), i32(), i32(), i32(), i32(), i32(), 1.0,
-                                  rnd.choice([0.0, 1.0]), rnd.choice([0, 2, 1, -1]), 0)
+                                  rnd.choice([0.0, 1.0]), rnd.choice([0, 2, 1, -1]), rnd.choice([0, 1, 2]))
         elif op == TRANSPOSE:
             payload = struct.pack("<QQiiiiII", h(), h(), i32(), i32(), i32(), i32(), small(), small())
         elif op == FILL:
@@ -297,3 +297,26 @@ def test_client_queue_flushes_at_64_frames(fuzz_bin, tmp_path):
     d.sock.close()
     stats = _finish(p)
     assert int(stats["frames"]) == 1 + 1 + 200 + 1
+
+
+def test_gemm_with_k_by_n_b_operand(fuzz_bin):
+    """GEMM flag bit 0: the second operand is B[K][N] (the [K][N] kernel):
+    its extent is K rows of ldb, not N rows -- a B that holds N*K elements
+    laid out [N][K] with a large ldb must not pass for [K][N]."""
+    A, B, C = 1 << 62, (1 << 62) + 1, (1 << 62) + 2
+    M, N, K = 4, 8, 16
+    frames = [
+        frame(ALLOC, struct.pack("<Q", M * K * 2)),
+        frame(ALLOC, struct.pack("<Q", K * N * 2)),
+        frame(ALLOC, struct.pack("<Q", M * N * 4)),
+        frame(GEMM, struct.pack("<QQQiiiiiiffii", A, B, C, M, N, K, K, N, N, 1.0, 0.0, 0, 1)),       # 3: fits
+        frame(GEMM, struct.pack("<QQQiiiiiiffii", A, B, C, M, N, K, K, N + 1, N, 1.0, 0.0, 0, 1)),   # 4: ldb past B
+        frame(GEMM, struct.pack("<QQQiiiiiiffii", A, B, C, M, N, K, K, 2**31 - 1, N, 1.0, 0.0, 0, 1)),  # 5: K*ldb huge
+        frame(GEMM, struct.pack("<QQQiiiiiiffii", A, B, C, M, N, K, K, N, N, 1.0, 0.0, 0, 2)),       # 6: unknown flag
+        frame(GEMM, struct.pack("<QQQiiiiiiffii", A, B, C, M, 2 * N, K // 2, K, K // 2, 2 * N, 1.0, 0.0, 0, 0)),  # 7: TN view of B
+    ]
+    rows = run(fuzz_bin, frames)
+    st = [r[1] for r in rows]
+    assert st[:4] == [OK] * 4, st
+    assert st[4:7] == [BAD_HANDLE] * 3, st
+    assert st[7] == BAD_HANDLE, st  # C is only M x N f32

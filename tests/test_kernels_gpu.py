@@ -535,3 +535,72 @@ def test_sum_mean_along_axis(gpu, dtype, shape):
     np.testing.assert_allclose(gpu.mean(x, axis=0).numpy().astype(np.float64), h.mean(axis=0), rtol=tol, atol=tol)
     # deterministic: same bits twice
     assert np.array_equal(gpu.sum(x, axis=0).numpy(), gpu.sum(x, axis=0).numpy())
+
+
+@pytest.mark.parametrize("shape", [(256, 256, 64), (512, 768, 320), (1024, 2048, 512), (4096, 4096, 4096)])
+@pytest.mark.parametrize("out", ["float32", "bfloat16"])
+@pytest.mark.parametrize("pad", [0, 64])
+def test_gemm_nn_kernel(gpu, shape, out, pad):
+    """C = A . B with B stored [K][N] (bk_gemm_bf16_nn: the 4-wave kernel
+    reading B through ds_read_b64_tr_b16 from an XOR-swizzled [k][n] LDS
+    image) against fp64, beta epilogue included, ldb > N."""
+    import torch
+
+    from bee_code_interpreter_fs_amd.ops import _native
+
+    M, N, K = shape
+    ldb = N + pad
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + pad)
+    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    bstore = torch.empty(K, ldb, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    b = bstore[:, :N]
+    dt = torch.float32 if out == "float32" else torch.bfloat16
+    c0 = torch.empty(M, N, device="cuda", dtype=dt).uniform_(-1, 1, generator=g)
+    c = c0.clone()
+    lib = _native.lib()
+    odt = 0 if out == "float32" else 2
+    assert lib.bk_gemm_bf16_nn_ok(a.data_ptr(), bstore.data_ptr(), c.data_ptr(), M, N, K, K, ldb, N, odt) == 1
+    rc = lib.bk_gemm_bf16_nn(a.data_ptr(), bstore.data_ptr(), c.data_ptr(), M, N, K, K, ldb, N, 0.75, 0.5, odt,
+                             torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = 0.75 * (a.double() @ b.double()) + 0.5 * c0.double()
+    tol = 1e-3 if out == "float32" else 4e-2
+    assert (c.double() - ref).abs().max().item() < tol * max(1.0, ref.abs().max().item())
+
+
+def test_gemm_nn_refuses_what_it_cannot_do(gpu):
+    import torch
+
+    from bee_code_interpreter_fs_amd.ops import _native
+
+    lib = _native.lib()
+    a = torch.zeros(300, 256, device="cuda", dtype=torch.bfloat16)
+    c = torch.zeros(300, 512, device="cuda", dtype=torch.float32)
+    s = torch.cuda.current_stream().cuda_stream
+    # M not a tile multiple; ldb < N
+    assert lib.bk_gemm_bf16_nn(a.data_ptr(), a.data_ptr(), c.data_ptr(), 300, 256, 256, 256, 256, 512, 1.0, 0.0, 0, s) == 1
+    assert lib.bk_gemm_bf16_nn(a.data_ptr(), a.data_ptr(), c.data_ptr(), 256, 512, 256, 256, 256, 512, 1.0, 0.0, 0, s) == 1
+
+
+@pytest.mark.parametrize("nn", [False, True])
+def test_matmul_row_major_b(gpu, nn, monkeypatch):
+    """bk.matmul(a, b) with a plain row-major bf16 b: transpose + TN, or
+    (BEE_GEMM_NN) the [K][N] kernel for tile-multiple shapes -- against fp64."""
+    import numpy as np
+
+    import sys
+
+    arr = sys.modules["bee_code_interpreter_fs_amd.ops.array"]  # (the package exports a function named array)
+    monkeypatch.setattr(arr, "_GEMM_NN", nn)
+    for M, N, K in ((4096, 4096, 1024), (300, 200, 136)):
+        rng = np.random.default_rng(M)
+        an = rng.uniform(-1, 1, (M, K)).astype(np.float32)
+        bn = rng.uniform(-1, 1, (K, N)).astype(np.float32)
+        a = gpu.asarray(an).astype("bfloat16")
+        b = gpu.asarray(bn).astype("bfloat16")
+        c = gpu.matmul(a, b, out_dtype="float32").numpy()
+        ab = a.astype("float32").numpy().astype(np.float64)
+        bb = b.astype("float32").numpy().astype(np.float64)
+        ref = ab @ bb
+        assert np.abs(c - ref).max() < 1e-3 * max(1.0, np.abs(ref).max()), (M, N, K)
