@@ -85,8 +85,8 @@ WORKLOADS = {
 def parse_args():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=30)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=300)  # per client: 2400 Executes on 1 GPU, ~1 s
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--concurrency", type=int, default=8, help="closed-loop clients per GPU")
     p.add_argument("--pool-target", type=int, default=16, help="warm minimal sandboxes per GPU")
     p.add_argument("--frontends", type=int, default=0, help="front-end replicas (0 = two per GPU, at most 16)")
