@@ -31,6 +31,9 @@ import time
 
 DEFAULT_PRELOAD = "numpy,pandas,scipy.stats,matplotlib.pyplot,PIL.Image,torch,bee_code_interpreter_fs_amd.ops"
 PR_SET_CHILD_SUBREAPER = 36
+# environment entries every spawn message carries (csrc/executor/sandbox.cpp spawn_worker)
+_SPAWN_ENV_KEYS = ("BEE_WORKER_ID", "BEE_SANDBOX_DIR", "BEE_WORKSPACE", "BEE_RUNTIME_PACKAGES", "BEE_META_DIR",
+                   "TMPDIR", "HOME")
 PR_SET_DUMPABLE = 4
 
 
@@ -182,6 +185,11 @@ def main() -> None:
     n_rules = jail.prepare()  # the sandboxes' filesystem view, resolved once
     if n_rules is not None:
         loaded.append(f"jail:{n_rules}-rules")
+    # every spawn sets these: give them a slot in both environment views now,
+    # so a sandbox replaces values instead of growing libc's environ array
+    # and resizing os.environ's dict (copy-on-write faults in every sandbox)
+    for k in _SPAWN_ENV_KEYS:
+        os.environ.setdefault(k, "")
     _freeze_for_fork()
     if thp_on:
         collapsed, _ = thp.thp_collapse()
