@@ -274,9 +274,9 @@ def test_client_batches_launches_into_one_send(fuzz_bin, tmp_path):
     d.flush()
     d.sock.close()
     stats = _finish(p)
-    assert int(stats["frames"]) == 1 + 8 + 8 + 1 + 1 + 1 + 1 + 1 + 1 + 1
-    assert int(stats["replies"]) == 5            # HELLO, 2x READ, WRITE, SYNC
-    # HELLO, the 17-frame batch, 1 MiB WRITE (chunked reads), READ, copy+sync, free: far fewer reads than frames
+    assert int(stats["frames"]) == 8 + 8 + 1 + 1 + 1 + 1 + 1 + 1 + 1  # (no HELLO: connect is enough)
+    assert int(stats["replies"]) == 4            # 2x READ, WRITE, SYNC
+    # the 17-frame batch, 1 MiB WRITE (chunked reads), READ, copy+sync, free: far fewer reads than frames
     assert int(stats["reads"]) < int(stats["frames"])
     assert stats["live"] == "0"
 
@@ -288,6 +288,7 @@ def test_client_queue_flushes_at_64_frames(fuzz_bin, tmp_path):
     p = _serve(fuzz_bin, path)
     d = BrokerDriver(path)
     d.init(0)
+    assert d.hello()["arch"] == "host-fuzz"
     h = d.malloc(1 << 12)
     for _ in range(200):
         d.fill(h, 1 << 12, 7, 8)
@@ -296,7 +297,7 @@ def test_client_queue_flushes_at_64_frames(fuzz_bin, tmp_path):
     assert d._out_frames == 0 and not d._out
     d.sock.close()
     stats = _finish(p)
-    assert int(stats["frames"]) == 1 + 1 + 200 + 1
+    assert int(stats["frames"]) == 1 + 1 + 200 + 1  # HELLO (asked for), ALLOC_AT, 200 FILL, SYNC
 
 
 def test_gemm_with_k_by_n_b_operand(fuzz_bin):
