@@ -97,8 +97,7 @@ class CodeInterpreterServicer:
             await context.abort(grpc.StatusCode.INTERNAL, f"execution failed: {e}")
         METRICS.inc("bee_rpc_total", rpc="Execute", code="OK")
         METRICS.observe_ms("bee_rpc_latency_ms", (time.perf_counter() - t0) * 1e3, rpc="Execute")
-        for phase, ms in result.timings_ms.items():
-            METRICS.observe_ms("bee_execute_phase_ms", ms, phase=phase)
+        METRICS.observe_phases("bee_execute_phase_ms", result.timings_ms)
         logger.info("Code execution completed with exit code %s", result.exit_code)
         return pb.ExecuteResponse(
             stdout=result.stdout,

@@ -184,8 +184,7 @@ def create_http_server(code_executor, custom_tool_executor: CustomToolExecutor, 
         except Exception as e:
             logger.exception("Error executing code")
             raise HTTPException(status_code=500, detail=str(e))
-        for phase, ms in result.timings_ms.items():
-            METRICS.observe_ms("bee_execute_phase_ms", ms, phase=phase)
+        METRICS.observe_phases("bee_execute_phase_ms", result.timings_ms)
         return ExecuteResponse(
             stdout=result.stdout,
             stderr=result.stderr,

@@ -30,6 +30,7 @@ class Histogram:
 class Metrics:
     def __init__(self) -> None:
         self._lock = threading.Lock()
+        self._phase_keys: dict = {}
         self.counters: Dict[Tuple[str, Tuple], float] = defaultdict(float)
         self.hists: Dict[Tuple[str, Tuple], Histogram] = {}
 
@@ -44,6 +45,20 @@ class Metrics:
             if h is None:
                 h = self.hists[key] = Histogram()
             h.observe(value_ms)
+
+    def observe_phases(self, name: str, timings_ms: dict, label: str = "phase") -> None:
+        """observe_ms for every (phase, ms) of one request under one lock,
+        with the label keys cached (called on every Execute)."""
+        cache = self._phase_keys
+        with self._lock:
+            for phase, ms in timings_ms.items():
+                key = cache.get((name, label, phase))
+                if key is None:
+                    key = cache[(name, label, phase)] = (name, ((label, phase),))
+                h = self.hists.get(key)
+                if h is None:
+                    h = self.hists[key] = Histogram()
+                h.observe(ms)
 
     def render(self) -> str:
         lines = []
