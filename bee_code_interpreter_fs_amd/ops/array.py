@@ -537,11 +537,11 @@ def power(a, b): return _binary("power", a, b)
 
 # ---- matmul --------------------------------------------------------------------------
 
-# The [K][N] kernel (bk_gemm_bf16_nn) is correct but not yet faster than
-# transpose + TN: the compiler puts an s_waitcnt vmcnt(0) before every
-# ds_read_b64_tr_b16 (the intrinsic's memory operand defeats the LDS-DMA alias
-# check), serialising its B reads behind the in-flight tile loads -- 595 vs
-# 1193 TFLOP/s at 4096^3 (profiles/r2_gemm_nn_bench.log).  Opt-in until then.
+# The [K][N] kernel (bk_gemm_bf16_nn) reads B in place: 1066 / 1330 / 1221
+# TFLOP/s at 4096^3 / 8192^3 / 4096x8192x2048, 96-98% of hipBLASLt's NN
+# product; transpose + TN is 1144 / 1363 / 1170 on the same box
+# (profiles/r2_gemm_nn_bench_rawglds.log) -- ahead on square shapes, behind
+# on short K.  Opt-in until one wins everywhere.
 _GEMM_NN = os.environ.get("BEE_GEMM_NN", "0") == "1"
 
 

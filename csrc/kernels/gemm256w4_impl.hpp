@@ -116,7 +116,35 @@ struct Panel {
                     // (kNN B panels: 4 variants, see make_panel_nn)
   int row_bytes;    // ld * 2
   int k_lim[2];     // kEdge: this lane's chunk holds K columns while k0 < k_lim (K - 8 * chunk)
+  __attribute__((ext_vector_type(4))) unsigned w;  // kNN: the same descriptor as 4 SGPR words (glds_raw)
 };
+
+typedef __attribute__((ext_vector_type(4))) unsigned srd4;
+
+// a raw buffer descriptor's words (what __builtin_amdgcn_make_buffer_rsrc
+// builds with stride 0 and these flags), wave-uniform
+__device__ __forceinline__ srd4 srd_words(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  srd4 w;
+  w.x = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  w.y = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  w.z = __builtin_amdgcn_readfirstlane(bytes);
+  w.w = 0x00020000u;
+  return w;
+}
+
+// buffer_load_dwordx4 ... lds written as inline asm.  The kNN kernel issues
+// its direct-to-LDS loads this way because the compiler, seeing an LDS DMA in
+// flight, puts an s_waitcnt vmcnt(0) before every ds_read_b64_tr_b16 (whose
+// memory operand it cannot disambiguate) -- 14x the wait cycles
+// (profiles/r2_gemm_pmc_4096.jsonl).  Hidden from the compiler, the loads are
+// ordered by the schedule's own s_waitcnt vmcnt + s_barrier, as before.
+__device__ __forceinline__ void glds_raw(const srd4& w, const uint16_t* lds, int voff, int soff) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(lds_void_ptr)(lds));
+  const int so = __builtin_amdgcn_readfirstlane(soff);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0), "v"(voff), "s"(w), "s"(so)
+               : "memory", "m0");
+}
 
 __device__ __forceinline__ Panel make_panel(const uint16_t* base, int ld, int lane, int rows = 256, int K = 0) {
   Panel p;
@@ -162,6 +190,7 @@ __device__ __forceinline__ Panel make_panel_nn(const uint16_t* base, int ld, int
   const int64_t span = (int64_t)K * ld * 2;
   const uint32_t bytes = __builtin_amdgcn_readfirstlane(span > 0xffffffffll ? 0xffffffffu : (uint32_t)span);
   p.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+  p.w = srd_words(base, bytes);
   p.row_bytes = ld * 2;
   const int b = lane >> 5, pos16 = lane & 31;
   // glds instruction i of a wave fills LDS rows 2*(8*wave + i) + b; f of
@@ -179,8 +208,13 @@ __device__ __forceinline__ Panel make_panel_nn(const uint16_t* base, int ld, int
 
 __device__ __forceinline__ void glds_nn(const Panel& p, int k0, uint16_t* lds_operand, int wave, int i) {
   const int soff = (k0 + (wave * 8 + i) * 2) * p.row_bytes;
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(p.rsrc, (lds_void_ptr)(lds_operand + (wave * kGlds + i) * 8 * TK), 16,
-                                           p.lane_off[(i & 1) | ((i >> 2) << 1)], soff, 0, 0);
+  glds_raw(p.w, lds_operand + (wave * kGlds + i) * 8 * TK, p.lane_off[(i & 1) | ((i >> 2) << 1)], soff);
+}
+
+// the A operand's glds of a kNN kernel (same addressing as glds_one), raw
+__device__ __forceinline__ void glds_a_raw(const Panel& p, int k0, uint16_t* lds_operand, int wave, int i) {
+  const int soff = (wave * 64 + i * 8) * p.row_bytes + k0 * 2;
+  glds_raw(p.w, lds_operand + (wave * kGlds + i) * 8 * TK, p.lane_off[i & 1], soff);
 }
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -213,10 +247,15 @@ __device__ __forceinline__ int chunk_off(const Panel& p, int k0, int par, bool k
 // stage one operand's K-tile: 8 wave-instructions of 1 KiB (8 rows) each;
 // `wave` must be wave-uniform (readfirstlane'd) so the LDS base goes to M0
 __device__ __forceinline__ void stage(const Panel& p, int k0, uint16_t* lds_operand, int wave, bool kt = false,
-                                      bool nn = false) {
+                                      bool nn = false, bool raw_a = false) {
   if (nn) {
 #pragma unroll
     for (int i = 0; i < kGlds; ++i) glds_nn(p, k0, lds_operand, wave, i);
+    return;
+  }
+  if (raw_a) {
+#pragma unroll
+    for (int i = 0; i < kGlds; ++i) glds_a_raw(p, k0, lds_operand, wave, i);
     return;
   }
 #pragma unroll
@@ -344,12 +383,16 @@ __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], 
     for (int jj = 0; jj < 4; ++jj) mfma_asm<false>(acc[g >> 1][(g & 1) * 4 + jj], fa1[g >> 1], fb1[(g & 1) * 4 + jj]);
     if constexpr (EARLY) {  // all 16 glds in the first 8 groups: more time to land
       if (g < 8) {
-        glds_one(pa, kn, cur, wave, g, KT);
+        if constexpr (NN) glds_a_raw(pa, kn, cur, wave, g);
+        else glds_one(pa, kn, cur, wave, g, KT);
         if constexpr (NN) glds_nn(pb, kn, cur + kOperand, wave, g);
         else glds_one(pb, kn, cur + kOperand, wave, g, KT);
       }
     } else {
-      if (g < 8) glds_one(pa, kn, cur, wave, g, KT);
+      if (g < 8) {
+        if constexpr (NN) glds_a_raw(pa, kn, cur, wave, g);
+        else glds_one(pa, kn, cur, wave, g, KT);
+      }
       else if constexpr (NN) glds_nn(pb, kn, cur + kOperand, wave, g - 8);
       else glds_one(pb, kn, cur + kOperand, wave, g - 8, KT);
     }
@@ -480,7 +523,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 1, wc = wave & 1;
-  const Panel pa = make_panel(A + (int64_t)m0 * lda, lda, lane, edge ? min(TM, M - m0) : TM, K);
+  Panel pa = make_panel(A + (int64_t)m0 * lda, lda, lane, edge ? min(TM, M - m0) : TM, K);
+  if constexpr (nn) {
+    const int64_t span = (int64_t)TM * lda * 2;
+    pa.w = srd_words(A + (int64_t)m0 * lda, span > 0xffffffffll ? 0xffffffffu : (uint32_t)span);
+  }
   const Panel pb = nn ? make_panel_nn(Bt + n0, ldb, lane, K)
                       : make_panel(Bt + (int64_t)n0 * ldb, ldb, lane, edge ? min(TN, N - n0) : TN, K);
 
@@ -492,10 +539,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
 
   const int nk = edge ? (K + TK - 1) / TK : K / TK;  // kEdge: a ragged last K-tile reads zeros past K
   // prologue: tiles 0 and 1 in flight, wait for tile 0 (16 glds per tile)
-  stage(pa, 0, smem, wave, edge);
+  stage(pa, 0, smem, wave, edge, false, nn);
   stage(pb, 0, smem + kOperand, wave, edge, nn);
   if (nk > 1) {
-    stage(pa, TK, smem + kBuf, wave, edge);
+    stage(pa, TK, smem + kBuf, wave, edge, false, nn);
     stage(pb, TK, smem + kBuf + kOperand, wave, edge, nn);
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   } else {
@@ -522,7 +569,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       barrier();
       const int kn = min(t + 2, nk - 1) * TK;
-      stage(pa, kn, cur, wave, edge);
+      stage(pa, kn, cur, wave, edge, false, nn);
       stage(pb, kn, cur + kOperand, wave, edge, nn);
     }
   } else {
@@ -544,7 +591,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
     // the end, re-stage the last K-tile into the buffer nobody reads again
     // and read fragments nobody uses
     const int kn = min(t + 2, nk - 1) * TK;
-    stage(pa, kn, cur, wave, edge);
+    stage(pa, kn, cur, wave, edge, false, nn);
     stage(pb, kn, cur + kOperand, wave, edge, nn);
     read_frags(nxt, wr, wc, lane, 0, fa0, fb0, nn);
     if constexpr (inter) interleave_hint<16, 16>();
