@@ -387,7 +387,7 @@ def gang_allreduce_check(target, n):
     try:
         with grpc.insecure_channel(target) as ch:
             r = pb.CodeInterpreterServiceStub(ch).Execute(
-                pb.ExecuteRequest(source_code=GANG_SCRIPT, gpus=n, timeout=240), timeout=300
+                pb.ExecuteRequest(source_code=GANG_SCRIPT, gpus=n, timeout=120), timeout=150
             )
         line = [l for l in r.stdout.splitlines() if l.startswith("allreduce_ok")]
         out = {"exit_code": r.exit_code, "result": line[0] if line else None,
