@@ -81,6 +81,50 @@ def _open_outputs(meta_dir: str) -> None:
         _OUT_FDS[name] = os.open(os.path.join(meta_dir, name), flags, 0o600)
 
 
+_STDIO: Optional[tuple] = None  # (stdin, stdout, stderr) text layers over fds 0/1/2, built by the zygote
+
+
+def prepare_stdio() -> None:
+    """Zygote, before forking: the text layers a `python script.py` run has
+    over fds 0/1/2, built once (closefd=False, empty buffers at the fork) and
+    installed as the zygote's own sys.std*, so a sandbox only points the
+    descriptors at its run's files.  Building them per sandbox -- three
+    FileIO / BufferedWriter / TextIOWrapper stacks, codec lookups, and the
+    deallocation of the zygote's layers they replaced -- measured 0.2 ms and
+    ~110 copy-on-write faults of every sandbox's CPU on MI355X.  Built while
+    fds 0/1/2 point at /dev/null, so the layers see what a run's regular
+    files look like (seekable, position 0)."""
+    global _STDIO
+    for stream in (sys.stdout, sys.stderr):
+        try:
+            stream.flush()
+        except Exception:
+            pass
+    null_fd = os.open(os.devnull, os.O_RDWR)
+    saved = [os.dup(fd) for fd in (0, 1, 2)]
+    try:
+        for fd in (0, 1, 2):
+            os.dup2(null_fd, fd)
+        stdin = io.TextIOWrapper(io.FileIO(0, "r", closefd=False), encoding="utf-8")
+        stdout = io.TextIOWrapper(
+            io.BufferedWriter(io.FileIO(1, "w", closefd=False)), encoding="utf-8", errors="backslashreplace"
+        )
+        stderr = io.TextIOWrapper(
+            io.BufferedWriter(io.FileIO(2, "w", closefd=False)),
+            encoding="utf-8",
+            errors="backslashreplace",
+            line_buffering=True,
+        )
+    finally:
+        for fd, keep in zip((0, 1, 2), saved):
+            os.dup2(keep, fd)
+            os.close(keep)
+        os.close(null_fd)
+    _STDIO = (stdin, stdout, stderr)
+    sys.stdin, sys.stdout, sys.stderr = _STDIO
+    sys.__stdin__, sys.__stdout__, sys.__stderr__ = _STDIO
+
+
 def _redirect_stdio(stdout_path: str, stderr_path: str) -> None:
     flags = os.O_WRONLY | os.O_CREAT | os.O_TRUNC
     out_fd = _OUT_FDS.pop("stdout", None)
@@ -96,6 +140,13 @@ def _redirect_stdio(stdout_path: str, stderr_path: str) -> None:
     os.dup2(err_fd, 2)
     for fd in (out_fd, err_fd, null_fd):
         os.close(fd)
+    if _STDIO is not None and not _STDIO[1].closed and not _STDIO[2].closed:
+        # the zygote's layers (prepare_stdio): nothing buffered, now over the run's files
+        for stream in _STDIO[1:]:
+            stream.flush()
+        sys.stdin, sys.stdout, sys.stderr = _STDIO
+        sys.__stdin__, sys.__stdout__, sys.__stderr__ = _STDIO
+        return
     # fresh text layers like a normal `python script.py` writing to files
     sys.stdin = io.TextIOWrapper(io.FileIO(0, "r", closefd=False), encoding="utf-8")
     sys.stdout = io.TextIOWrapper(
@@ -518,11 +569,15 @@ def _serve(cwd: str, chan: _Chan) -> None:
         meta = os.environ.get("BEE_META_DIR", "")
         if meta and "stdout" in _OUT_FDS and "stderr" in _OUT_FDS:
             _redirect_stdio(os.path.join(meta, "stdout"), os.path.join(meta, "stderr"))
+        _cpu_stamp("redirect")
         rp = os.environ.get("BEE_RUNTIME_PACKAGES", "")
         ws_view, rp_view = _logical_view(cwd, rp)
+        _cpu_stamp("view")
         _prepare_paths(rp_view)
+        _cpu_stamp("paths")
         chan.send(('{"op":"ready","warm_ms":%.3f,"gpu_error":%s}\n'
                    % ((time.perf_counter() - t0) * 1e3, _json_str(gpu_error or ""))).encode())
+        _cpu_stamp("ready")
         job = chan.recv_json()
         if job is None or job.get("op") != "run":
             os._exit(0)

@@ -190,6 +190,9 @@ def main() -> None:
     # and resizing os.environ's dict (copy-on-write faults in every sandbox)
     for k in _SPAWN_ENV_KEYS:
         os.environ.setdefault(k, "")
+    from . import worker
+
+    worker.prepare_stdio()  # sandboxes reuse these text layers over fds 0/1/2
     _freeze_for_fork()
     if thp_on:
         collapsed, _ = thp.thp_collapse()

@@ -84,22 +84,44 @@ class HipDevice final : public broker::Device {
   // whole wait even under hipDeviceScheduleBlockingSync (measured on MI355X,
   // tools/probe/sync_cpu_probe.hip: a 150 us kernel cost 159 us of CPU in
   // hipStreamSynchronize, 7 us this way), and every reduce / read of every
-  // sandbox waits.  Checks 2 us apart at first, then every 10 us (the broker
-  // threads run with a 1 us timer slack): a request waits ~3 times, so the
-  // step bounds the latency it adds.  BEE_BROKER_WAIT=spin: HIP's wait.
+  // sandbox waits.  Checks 2 us apart at first, then each 1/8 of the time
+  // waited so far after the last (<= 50 us; the broker threads run with a
+  // 1 us timer slack): the checks grow geometrically and a wait overshoots by
+  // at most 1/8.  BEE_BROKER_POLL tunes it, BEE_BROKER_WAIT=spin: HIP's wait.
   bool wait(Ctx* c) {
     if (spin_wait_) return hipStreamSynchronize(c->s) == hipSuccess;
     if (!c->wait_ev && hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming) != hipSuccess)
       return hipStreamSynchronize(c->s) == hipSuccess;
     if (hipEventRecord(c->wait_ev, c->s) != hipSuccess) return false;
-    long ns = 2000;
+    long ns = poll_min_ns_;
+    const double t0 = poll_div_ > 0 ? mono_ms() : 0.0;
     for (;;) {
       const hipError_t e = hipEventQuery(c->wait_ev);
       if (e == hipSuccess) return true;
       if (e != hipErrorNotReady) return false;
       timespec ts{0, ns};
       nanosleep(&ts, nullptr);
-      if (ns < 10000) ns += 2000;
+      if (poll_div_ > 0) {  // the next check a fixed fraction of the wait so far away
+        const long rel = (long)((mono_ms() - t0) * 1e6 / poll_div_);
+        ns = rel < poll_min_ns_ ? poll_min_ns_ : rel > poll_max_ns_ ? poll_max_ns_ : rel;
+      } else if (ns < poll_max_ns_) {
+        ns += poll_min_ns_;
+      }
+    }
+  }
+
+  // BEE_BROKER_POLL=min_us,max_us[,div]: checks min_us apart at first, then
+  // growing by min_us up to max_us (div 0), or div > 0: each check 1/div of
+  // the time waited so far after the last, clamped to [min_us, max_us]
+  static void poll_schedule(long* min_ns, long* max_ns, int* div) {
+    const char* p = getenv("BEE_BROKER_POLL");
+    if (!p || !*p) return;
+    double a = 0, b = 0;
+    int d = 0;
+    if (sscanf(p, "%lf,%lf,%d", &a, &b, &d) >= 2 && a > 0 && b >= a && b <= 1e4 && d >= 0) {
+      *min_ns = (long)(a * 1e3);
+      *max_ns = (long)(b * 1e3);
+      *div = d;
     }
   }
 
@@ -308,6 +330,13 @@ class HipDevice final : public broker::Device {
 
  private:
   bool spin_wait_ = getenv("BEE_BROKER_WAIT") && !strcmp(getenv("BEE_BROKER_WAIT"), "spin");
+  // default: relative backoff (2 us, then 1/8 of the wait so far, <= 50 us):
+  // A/B on MI355X, 4 interleaved runs each, broker CPU 0.30-0.33 vs
+  // 0.34-0.35 ms per Execute, RPS 2500-2665 vs 2466-2550
+  // (profiles/r2_s3_broker_poll_ab.log)
+  long poll_min_ns_ = 2000, poll_max_ns_ = 50000;
+  int poll_div_ = 8;
+  bool poll_set_ = (poll_schedule(&poll_min_ns_, &poll_max_ns_, &poll_div_), true);
   void* lib_ = nullptr;
   std::string arch_;
   int64_t cus_ = 0, clock_ = 0, lds_ = 0;

@@ -22,8 +22,11 @@ a = bk.random.uniform(-1, 1, (4096, 4096), dtype="bfloat16"); t.append(time.perf
 b = bk.random.uniform(-1, 1, (4096, 4096), dtype="bfloat16"); t.append(time.perf_counter())
 c = bk.matmul(a, b.T); t.append(time.perf_counter())
 s = bk.sum(c); t.append(time.perf_counter())
+ref = bk.dot(bk.sum(a, axis=0), bk.sum(b, axis=0)); t.append(time.perf_counter())
+print("Result:", r, s, ref); t.append(time.perf_counter())
 del x, a, b, c; t.append(time.perf_counter())
-names = ["import", "rand_f64", "square_sum", "rand_bf16_a", "rand_bf16_b", "matmul", "sum_c", "free"]
+names = ["import", "rand_f64", "square_sum", "rand_bf16_a", "rand_bf16_b", "matmul", "sum_c", "colsum_dot", "print",
+         "free"]
 print("BREAKDOWN", {n: round((t[i + 1] - t[i]) * 1e3, 3) for i, n in enumerate(names)})
 '''
 
@@ -33,7 +36,7 @@ def main():
 
     ensure_native_executor()
     h = ServiceHarness(tempfile.mkdtemp(prefix="bee-bd-"), gpu_ids=[0], workers_per_gpu_target=1,
-                       light_workers_per_gpu_target=16, max_inflight_per_gpu=64, default_timeout=120.0)
+                       min_workers_per_gpu_target=16, light_workers_per_gpu_target=2, max_inflight_per_gpu=64, default_timeout=120.0)
     h.start()
     try:
         for conc in (1, 4, 8, 16):
