@@ -137,6 +137,15 @@ class ExecutorProcess:
         if self.gpus:
             # the daemon's own HIP context (kernel broker) lives on its GPU only
             env["HIP_VISIBLE_DEVICES"] = self.gpus
+            # BEE_EXECUTOR_HW_QUEUES: HIP hardware queues behind the kernel
+            # broker's per-session streams (GPU_MAX_HW_QUEUES of the daemon
+            # only; HIP reads it before main).  Left at the inherited value:
+            # on MI355X 2 queues cut the in-sandbox GPU time of 8 concurrent
+            # headline Executes from 1.04-1.12 to 0.93-0.96 ms, but moved
+            # neither RPS nor p50 beyond box noise (2503 vs 2580, 2437 vs 2329
+            # RPS means in two interleaved series; profiles/r2_s3_hw_queues_ab.log)
+            if os.environ.get("BEE_EXECUTOR_HW_QUEUES"):
+                env["GPU_MAX_HW_QUEUES"] = os.environ["BEE_EXECUTOR_HW_QUEUES"]
         self.log_path = os.path.join(run_dir, "executor.log")
         log = open(self.log_path, "ab")
         try:
