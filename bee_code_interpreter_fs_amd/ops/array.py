@@ -537,22 +537,34 @@ def power(a, b): return _binary("power", a, b)
 
 # ---- matmul --------------------------------------------------------------------------
 
-# The [K][N] kernel (bk_gemm_bf16_nn) reads B in place: 1066 / 1330 / 1221
-# TFLOP/s at 4096^3 / 8192^3 / 4096x8192x2048, 96-98% of hipBLASLt's NN
-# product; transpose + TN is 1144 / 1363 / 1170 on the same box
-# (profiles/r2_gemm_nn_bench_rawglds.log) -- ahead on square shapes, behind
-# on short K.  Opt-in until one wins everywhere.
-_GEMM_NN = os.environ.get("BEE_GEMM_NN", "0") == "1"
+# The [K][N] kernel (bk_gemm_bf16_nn) reads B in place; the alternative is a
+# transpose pass (4*K*N bytes of HBM traffic) then the TN kernel, which runs
+# 7-10% faster than the [K][N] one.  The pass costs ~600/M of the GEMM, so
+# reading in place wins below M ~ 6k.  Measured on MI355X, TFLOP/s, [K][N]
+# kernel vs transpose + TN (hipBLASLt's NN in brackets,
+# profiles/r2_s3_gemm_nn_sweep.log):
+#   M=N=4096,  K=512..4096: 715/949/1132/1229/1298 vs 574/771/1029/1154/1218
+#                           (659/935/1140/1256/1302)
+#   2048x8192x2048: 1211 vs 1014 (1195)
+#   M=N=8192,  K=1024..8192: 1081/1242/1286/1298 vs 1091/1252/1328/1325
+#   16384x4096x1024: 1104 vs 1108
+# BEE_GEMM_NN: auto (M below _NN_MAX_M), 1 (whenever the shape allows), 0 (never)
+_GEMM_NN = os.environ.get("BEE_GEMM_NN", "auto")
+_NN_MAX_M = 6144
+
+
+def _use_nn(M: int) -> bool:
+    return _GEMM_NN == "1" or (_GEMM_NN == "auto" and M < _NN_MAX_M)
 
 
 def matmul(a, b, out_dtype: str = "bfloat16") -> DeviceArray:
     """C = A @ B on the bf16 MFMA GEMM (f32 accumulate).
 
     ``b.T`` views of a row-major [N, K] buffer are used as is (the TN
-    kernels); a plain row-major ``b`` is transposed once on device (15 us at
-    4096^2) -- or, with BEE_GEMM_NN=1, read in place by the [K][N] kernel for
-    tile-multiple shapes; an f32/f64 ``b`` is converted and transposed in the
-    same pass.
+    kernels); a plain row-major bf16 ``b`` is read in place by the [K][N]
+    kernel for tile-multiple shapes with M below ~6k (BEE_GEMM_NN), else
+    transposed once on device (15 us at 4096^2) for the TN kernel; an f32/f64
+    ``b`` is converted and transposed in the same pass.
     """
     a = _as_operand(a)
     b = _as_operand(b)
@@ -585,7 +597,7 @@ def matmul(a, b, out_dtype: str = "bfloat16") -> DeviceArray:
         from .driver import nn_shape_ok
 
         d = driver()
-        if _GEMM_NN and hasattr(d, "gemm_nn") and nn_shape_ok(M, N, K, K, N, N, out_dtype == "bfloat16") and \
+        if _use_nn(M) and hasattr(d, "gemm_nn") and nn_shape_ok(M, N, K, K, N, N, out_dtype == "bfloat16") and \
                 (d.name == "broker" or (a.ptr % 16 == 0 and b.ptr % 16 == 0)):
             # B[K, N] read in place through transposed LDS reads: no transpose pass
             c = DeviceArray((M, N), out_dtype)

@@ -104,3 +104,30 @@ def test_wide_transposed_view_materialises_on_device(fake, dtype):
     x.T._materialize()
     code = DTYPE_CODES[dtype]
     assert fake.calls == [("transpose", 24, 40, code)]
+
+
+class FakeNNDriver(FakeDriver):
+    def gemm_nn(self, a, b, c, M, N, K, lda, ldb, ldc, alpha, beta, odt):
+        self.calls.append(("gemm_nn", M, N, K))
+
+
+@pytest.mark.parametrize("mode,M,expect", [
+    ("auto", 4096, ["gemm_nn"]),               # transpose pass ~15% of the GEMM at M=4096: read B in place
+    ("auto", 8192, ["transpose", "gemm"]),     # ~7% at M=8192: the faster TN kernel after the pass
+    ("1", 8192, ["gemm_nn"]),
+    ("0", 4096, ["transpose", "gemm"]),
+])
+def test_row_major_bf16_b_kernel_choice(monkeypatch, mode, M, expect):
+    d = FakeNNDriver("broker")
+    monkeypatch.setattr(arr, "_driver", d)
+    monkeypatch.setattr(arr, "_GEMM_NN", mode)
+    arr.matmul(arr.DeviceArray((M, 1024), "bfloat16"), arr.DeviceArray((1024, 4096), "bfloat16"))
+    assert _ops(d) == expect
+
+
+def test_row_major_bf16_b_off_tile_shape_is_transposed(monkeypatch):
+    d = FakeNNDriver("broker")
+    monkeypatch.setattr(arr, "_driver", d)
+    monkeypatch.setattr(arr, "_GEMM_NN", "auto")
+    arr.matmul(arr.DeviceArray((4000, 1024), "bfloat16"), arr.DeviceArray((1024, 4096), "bfloat16"))
+    assert _ops(d) == ["transpose", "gemm"]

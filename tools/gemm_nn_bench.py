@@ -25,7 +25,9 @@ def timeit(fn, iters=30):
     return e0.elapsed_time(e1) / iters
 
 
-for M, N, K in ((4096, 4096, 4096), (8192, 8192, 8192), (4096, 8192, 2048)):
+# shapes: argv[1] as JSON [[M, N, K], ...], default the three README shapes
+SHAPES = json.loads(sys.argv[1]) if len(sys.argv) > 1 else [[4096, 4096, 4096], [8192, 8192, 8192], [4096, 8192, 2048]]
+for M, N, K in SHAPES:
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     b = torch.randn(K, N, device="cuda", dtype=torch.bfloat16)
     bt = b.T.contiguous()

@@ -21,11 +21,13 @@ def main():
     ap.add_argument("--n", type=int, default=5)
     args = ap.parse_args()
     os.environ["BEE_DEBUG_NEW_MODULES"] = "1"
+    os.environ["BEE_DEBUG_BOOT"] = "1"  # the zygote's C bootstrap, per step (lands in the executor log)
     from tests.harness import ServiceHarness, ensure_native_executor
 
     ensure_native_executor()
     src = open(os.path.join(ROOT, "examples", "benchmark_numpy_gpu.py")).read()
-    h = ServiceHarness(tempfile.mkdtemp(prefix="bee-dbg-"), gpu_ids=[0], workers_per_gpu_target=1,
+    tmp = tempfile.mkdtemp(prefix="bee-dbg-")
+    h = ServiceHarness(tmp, gpu_ids=[0], workers_per_gpu_target=1,
                        min_workers_per_gpu_target=4, light_workers_per_gpu_target=1, default_timeout=120.0)
     h.start()
     try:
@@ -36,6 +38,12 @@ def main():
                               "timings": {k: round(v, 3) for k, v in sorted(r.timings_ms.items())}}), flush=True)
     finally:
         h.stop()
+        import glob
+
+        for log in glob.glob(os.path.join(tmp, "sandboxes", "*", ".run", "executor.log")):
+            boots = [l.strip() for l in open(log, errors="replace") if l.startswith("BOOT")]
+            for l in boots[-args.n:]:
+                print(l)
 
 
 if __name__ == "__main__":
