@@ -246,6 +246,7 @@ __global__ __launch_bounds__(256) void colsum_partial_v(const T* __restrict__ x,
 #pragma unroll
   for (int j = 0; j < V; ++j) acc[j] = 0.0;
   if (col0 < cols) {
+#pragma unroll 4
     for (int64_t r = r0 + g; r < r1; r += 4) {
       const V16<T> v = *reinterpret_cast<const V16<T>*>(x + r * ld + col0);
 #pragma unroll
@@ -269,10 +270,21 @@ __global__ __launch_bounds__(256) void colsum_final(const double* __restrict__ p
   __shared__ double s4[4][64];
   const int tx = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int64_t col = (int64_t)blockIdx.x * 64 + tx;
-  double s = 0.0;
-  if (col < cols)
-    for (int c = g; c < chunks; c += 4) s += part[(int64_t)c * cols + col];
-  s4[g][tx] = s;
+  // four independent chains (chunks c, c+4, c+8, c+12): the loads of one
+  // thread are in flight together instead of one HBM latency per chunk
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  if (col < cols) {
+    int c = g;
+    for (; c + 12 < chunks; c += 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] += part[(int64_t)(c + 4 * j) * cols + col];
+    }
+    // (at most three chunks left: c, c+4, c+8)
+    if (c < chunks) a[0] += part[(int64_t)c * cols + col];
+    if (c + 4 < chunks) a[1] += part[(int64_t)(c + 4) * cols + col];
+    if (c + 8 < chunks) a[2] += part[(int64_t)(c + 8) * cols + col];
+  }
+  s4[g][tx] = (a[0] + a[1]) + (a[2] + a[3]);
   __syncthreads();
   if (g == 0 && col < cols) out[col] = (TO)(((s4[0][tx] + s4[1][tx]) + (s4[2][tx] + s4[3][tx])) * scale);
 }
