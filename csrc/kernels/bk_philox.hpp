@@ -20,7 +20,11 @@ struct Philox {
       const uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
       const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
       const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-      c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+      // three-input XORs as ONE v_bitop3_b32 each (gfx950; truth table 0x96 =
+      // a ^ b ^ c): the compiler emitted two v_xor_b32 apiece, 74 of the 183
+      // instructions of rand_reduce_f64's two-Philox loop body
+      c = make_uint4(__builtin_amdgcn_bitop3_b32(hi1, c.y, k0, 0x96), lo1,
+                     __builtin_amdgcn_bitop3_b32(hi0, c.w, k1, 0x96), lo0);
       k0 += W0;
       k1 += W1;
     }

@@ -1,0 +1,39 @@
+"""Fused Philox -> (square) -> sum kernel alone (bk_rand_reduce, 1e8 f64 /
+f32 draws) and the materialised f64 draw, event-timed in one process:
+    python tools/probe/rand_reduce_bench.py"""
+import ctypes
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from bee_code_interpreter_fs_amd.ops import _native  # noqa: E402
+
+lib = _native.lib()
+s = torch.cuda.current_stream().cuda_stream
+rr = lib.bk_rand_reduce
+rr.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
+               ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+ws = torch.empty(lib.bk_reduce_workspace_bytes() // 8 + 1, dtype=torch.float64, device="cuda")
+out = torch.empty(1, dtype=torch.float64, device="cuda")
+
+
+def timeit(fn, iters=50):
+    for _ in range(5):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+n = 10**8
+for op, dt, name in ((1, 1, "square_sum f64"), (0, 1, "sum f64"), (1, 0, "square_sum f32")):
+    us = timeit(lambda: rr(op, dt, n, 1234, 0, 0.0, 1.0, ws.data_ptr(), out.data_ptr(), s))
+    torch.cuda.synchronize()
+    print(json.dumps({"kernel": "bk_rand_reduce " + name, "n": n, "us": round(us, 2), "value": out.item(),
+                      "expect": n / 3 if op == 1 else n / 2}), flush=True)
