@@ -7,7 +7,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))))
 from bee_code_interpreter_fs_amd.ops import _native  # noqa: E402
 
 lib = _native.lib()
