@@ -197,6 +197,16 @@ def main() -> None:
     if thp_on:
         collapsed, _ = thp.thp_collapse()
         loaded.append(f"thp:{collapsed >> 20}MB")
+    if os.environ.get("BEE_DEBUG_ZYGOTE_MEM") == "1":  # what every fork copies / every exit tears down
+        try:
+            with open("/proc/self/smaps_rollup") as fh:
+                roll = " ".join(l.split(":")[0] + "=" + l.split()[1] for l in fh if l.split()[-1] == "kB")
+            with open("/proc/self/maps") as fh:
+                vmas = sum(1 for _ in fh)
+            sys.stderr.write(f"ZYGOTE_MEM kind={os.environ.get('BEE_ZYGOTE_KIND', '')} vmas={vmas} {roll}\n")
+            sys.stderr.flush()
+        except OSError:
+            pass
     try:
         libc = ctypes.CDLL(None)
         libc.prctl(PR_SET_CHILD_SUBREAPER, 1, 0, 0, 0)

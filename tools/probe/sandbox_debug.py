@@ -22,6 +22,7 @@ def main():
     args = ap.parse_args()
     os.environ["BEE_DEBUG_NEW_MODULES"] = "1"
     os.environ["BEE_DEBUG_BOOT"] = "1"  # the zygote's C bootstrap, per step (lands in the executor log)
+    os.environ["BEE_DEBUG_ZYGOTE_MEM"] = "1"  # each zygote's memory rollup (executor log)
     from tests.harness import ServiceHarness, ensure_native_executor
 
     ensure_native_executor()
@@ -41,7 +42,11 @@ def main():
         import glob
 
         for log in glob.glob(os.path.join(tmp, "sandboxes", "*", ".run", "executor.log")):
-            boots = [l.strip() for l in open(log, errors="replace") if l.startswith("BOOT")]
+            lines = list(open(log, errors="replace"))
+            for l in lines:
+                if l.startswith("ZYGOTE_MEM"):
+                    print(l.strip())
+            boots = [l.strip() for l in lines if l.startswith("BOOT")]
             for l in boots[-args.n:]:
                 print(l)
 
