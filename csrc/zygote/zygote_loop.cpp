@@ -21,6 +21,7 @@
 #include <Python.h>
 
 #include <errno.h>
+#include <malloc.h>
 #include <fcntl.h>
 #include <poll.h>
 #include <signal.h>
@@ -121,6 +122,17 @@ PyObject* thp_arenas(PyObject*, PyObject* args) {
   }
   g_arena.base = base;
   g_arena.size = reserve;
+  // glibc's own allocations the preload makes: from the heap, not from
+  // separate sub-2 MB mmaps (malloc's default for >= 128 KiB) that no huge
+  // page can cover -- the heap is one growing mapping thp_collapse() folds
+  // into 2 MB pages (measured: 4-8 MB of a minimal zygote's 14.7 MB of
+  // anonymous memory sat in 1-2 MB mmaps on 4 KB pages)
+  // (BEE_ZYGOTE_MALLOPT=0: glibc's defaults)
+  const char* mo = getenv("BEE_ZYGOTE_MALLOPT");
+  if (!mo || strcmp(mo, "0") != 0) {
+    mallopt(M_MMAP_THRESHOLD, 64 << 20);
+    mallopt(M_TOP_PAD, 2 << 20);
+  }
   PyObject_GetArenaAllocator(&g_arena.prev);
   PyObjectArenaAllocator a{nullptr, arena_alloc, arena_free};
   PyObject_SetArenaAllocator(&a);
@@ -157,7 +169,17 @@ PyObject* thp_collapse(PyObject*, PyObject*) {
     memcpy(&r, ranges.data() + i, sizeof r);
     for (uintptr_t p = r.a; p < r.b; p += kHuge) {
       tried += kHuge;
-      if (madvise((void*)p, kHuge, MADV_COLLAPSE) == 0) ok += kHuge;  // EINVAL/EAGAIN: empty or busy
+      // EINVAL: nothing to collapse there; EAGAIN: a transient shortage
+      // (no free huge page right now, a page briefly pinned) -- retried, as
+      // every 2 MB left on small pages is 512 entries each fork copies
+      for (int attempt = 0; attempt < 4; ++attempt) {
+        if (madvise((void*)p, kHuge, MADV_COLLAPSE) == 0) {
+          ok += kHuge;
+          break;
+        }
+        if (errno != EAGAIN) break;
+        usleep(200);
+      }
     }
   }
   return Py_BuildValue("(KK)", ok, tried);
