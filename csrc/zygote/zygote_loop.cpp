@@ -73,6 +73,7 @@ struct ArenaRegion {
   size_t arenas = 0, fallbacks = 0;
   PyObjectArenaAllocator prev{};
 } g_arena;
+bool g_malloc_tuned = false;  // thp_arenas raised glibc's mmap threshold / top pad
 
 void* arena_alloc(void*, size_t n) {
   ArenaRegion& r = g_arena;
@@ -132,6 +133,7 @@ PyObject* thp_arenas(PyObject*, PyObject* args) {
   if (!mo || strcmp(mo, "0") != 0) {
     mallopt(M_MMAP_THRESHOLD, 64 << 20);
     mallopt(M_TOP_PAD, 2 << 20);
+    g_malloc_tuned = true;
   }
   PyObject_GetArenaAllocator(&g_arena.prev);
   PyObjectArenaAllocator a{nullptr, arena_alloc, arena_free};
@@ -195,6 +197,13 @@ PyObject* thp_stats(PyObject*, PyObject*) {
 // should not fault in 2 MB at a time); the inherited huge pages stay
 void thp_child() {
   if (g_arena.base) madvise(g_arena.base, g_arena.size, MADV_NOHUGEPAGE);
+  // and glibc's usual thresholds again (thp_arenas raised them for the
+  // preload): a sandbox's large buffers are mmap'd and returned on free, as
+  // in a fresh interpreter
+  if (g_malloc_tuned) {
+    mallopt(M_MMAP_THRESHOLD, 128 << 10);
+    mallopt(M_TOP_PAD, 128 << 10);
+  }
 }
 
 double mono_s() {
