@@ -85,8 +85,11 @@ WORKLOADS = {
 def parse_args():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=300)  # per client: 2400 Executes on 1 GPU, ~1 s
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=600)  # per client: 4800 Executes on 1 GPU, ~2 s
+    # untimed: 400 Executes on 1 GPU bring the allocator caches, sandbox
+    # pools and zygote page state to steady state (30 timed steps after 10
+    # warm-up steps ran at 1836 RPS vs ~2700 sustained, profiles/r2_s3_bench_suite.jsonl)
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--concurrency", type=int, default=8, help="closed-loop clients per GPU")
     p.add_argument("--pool-target", type=int, default=16, help="warm minimal sandboxes per GPU")
     p.add_argument("--frontends", type=int, default=0, help="front-end replicas (0 = two per GPU, at most 16)")
