@@ -204,6 +204,20 @@ def main() -> None:
             with open("/proc/self/maps") as fh:
                 vmas = sum(1 for _ in fh)
             sys.stderr.write(f"ZYGOTE_MEM kind={os.environ.get('BEE_ZYGOTE_KIND', '')} vmas={vmas} {roll}\n")
+            # anonymous memory on small pages by mapping (>= 256 KiB of it)
+            cur, big = None, []
+            with open("/proc/self/smaps") as fh:
+                for line in fh:
+                    f = line.split()
+                    if f and "-" in f[0] and not f[0].endswith(":"):
+                        cur = {"range": f[0], "name": f[5] if len(f) > 5 else ""}
+                        big.append(cur)
+                    elif cur is not None and f and f[0] in ("Anonymous:", "AnonHugePages:"):
+                        cur[f[0][:-1]] = int(f[1])
+            small = [(m.get("Anonymous", 0) - m.get("AnonHugePages", 0), m["range"], m["name"]) for m in big]
+            for kb, rng, name in sorted(small, reverse=True)[:8]:
+                if kb >= 256:
+                    sys.stderr.write(f"ZYGOTE_MEM_SMALL {kb}kB {rng} {name}\n")
             sys.stderr.flush()
         except OSError:
             pass

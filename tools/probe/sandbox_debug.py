@@ -44,7 +44,7 @@ def main():
         for log in glob.glob(os.path.join(tmp, "sandboxes", "*", ".run", "executor.log")):
             lines = list(open(log, errors="replace"))
             for l in lines:
-                if l.startswith("ZYGOTE_MEM"):
+                if l.startswith("ZYGOTE_MEM"):  # (and ZYGOTE_MEM_SMALL)
                     print(l.strip())
             boots = [l.strip() for l in lines if l.startswith("BOOT")]
             for l in boots[-args.n:]:
