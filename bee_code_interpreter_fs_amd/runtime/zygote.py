@@ -168,6 +168,10 @@ def _thp_module():
 
 
 def main() -> None:
+    # the preloaded shim's early huge-page arenas (csrc/fsmap/zygote_thp.cpp)
+    # are this process's business only: sandboxes and their exec'd programs
+    # must not see the request
+    os.environ.pop("BEE_ZYGOTE_THP_EARLY", None)
     fd = int(os.environ["BEE_ZYGOTE_FD"])
     chan = socket.socket(fileno=fd)
     t0 = time.perf_counter()

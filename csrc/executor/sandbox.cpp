@@ -317,6 +317,10 @@ bool SandboxPool::start_zygote(Zygote* z, std::string* err) {
     for (auto& p : cfg_.protect) prot += ":" + p;
     env_store.push_back("BEE_JAIL_PROTECT=" + prot);
   }
+  // pymalloc arenas on huge pages from interpreter start-up on (the
+  // preloaded shim's constructor, csrc/fsmap/zygote_thp.cpp); an executor
+  // environment's BEE_ZYGOTE_THP_EARLY (e.g. 0) is passed on as is instead
+  if (!cfg_.zygote_preload.empty() && !getenv("BEE_ZYGOTE_THP_EARLY")) env_store.push_back("BEE_ZYGOTE_THP_EARLY=1");
   if (z->kind == kLight) env_store.push_back("BEE_PRELOAD=" + cfg_.light_preload);
   if (z->kind == kMin) env_store.push_back("BEE_PRELOAD=" + cfg_.min_preload);
   if (!cfg_.pythonpath.empty()) {

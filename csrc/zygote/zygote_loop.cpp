@@ -20,6 +20,7 @@
 // live sandbox's are killed (single-use sandboxes; zygote.py kill_escapees).
 #include <Python.h>
 
+#include <dlfcn.h>
 #include <errno.h>
 #include <malloc.h>
 #include <fcntl.h>
@@ -104,10 +105,30 @@ void arena_free(void*, void* p, size_t n) {
   munmap(p, n);  // arenas from before the switch, or fallbacks: plain mmaps
 }
 
+// the region the preloaded shim installed before the interpreter started
+// (csrc/fsmap/zygote_thp.cpp, same layout)
+struct BeeThpRegion {
+  char* base;
+  size_t size, used;
+  void* freed[1024];
+  size_t nfreed;
+  size_t arenas, fallbacks;
+};
+BeeThpRegion* g_early = nullptr;
+
 PyObject* thp_arenas(PyObject*, PyObject* args) {
   unsigned long long reserve = 1ull << 30;
   if (!PyArg_ParseTuple(args, "|K", &reserve)) return nullptr;
   if (g_arena.base) Py_RETURN_TRUE;
+  if (auto get = (BeeThpRegion * (*)()) dlsym(RTLD_DEFAULT, "bee_thp_region")) {
+    if (BeeThpRegion* r = get()) {  // arenas already there since start-up: adopt it
+      g_early = r;
+      g_arena.base = r->base;
+      g_arena.size = r->size;
+      g_malloc_tuned = true;  // (the shim raised glibc's thresholds too)
+      Py_RETURN_TRUE;
+    }
+  }
   reserve = (reserve + kHuge - 1) & ~(unsigned long long)(kHuge - 1);
   // over-map by one huge page and trim to 2 MB alignment
   char* raw = (char*)mmap(nullptr, reserve + kHuge, PROT_READ | PROT_WRITE,
@@ -188,6 +209,10 @@ PyObject* thp_collapse(PyObject*, PyObject*) {
 }
 
 PyObject* thp_stats(PyObject*, PyObject*) {
+  if (g_early)
+    return Py_BuildValue("{s:K,s:K,s:K,s:K,s:O}", "reserved", (unsigned long long)g_early->size, "used",
+                         (unsigned long long)g_early->used, "arenas", (unsigned long long)g_early->arenas, "fallbacks",
+                         (unsigned long long)g_early->fallbacks, "early", Py_True);
   return Py_BuildValue("{s:K,s:K,s:K,s:K}", "reserved", (unsigned long long)g_arena.size, "used",
                        (unsigned long long)g_arena.used, "arenas", (unsigned long long)g_arena.arenas, "fallbacks",
                        (unsigned long long)g_arena.fallbacks);
