@@ -92,7 +92,7 @@ def parse_args():
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--concurrency", type=int, default=8, help="closed-loop clients per GPU")
     p.add_argument("--pool-target", type=int, default=16, help="warm minimal sandboxes per GPU")
-    p.add_argument("--frontends", type=int, default=0, help="front-end replicas (0 = two per GPU, at most 16)")
+    p.add_argument("--frontends", type=int, default=0, help="front-end replicas (0 = three per GPU, at most 16)")
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="numpy_gpu")
     p.add_argument("--payload", default=None, help="override the workload's script")
     p.add_argument("--cpu-only", action="store_true", help="executors without GPUs (BASELINE config 1)")
@@ -215,10 +215,12 @@ def gpu_ids(n_gpus: int, args):
 
 def start_service(tmp: str, n_gpus: int, args):
     gport, hport = free_port(), free_port()
-    # two front-end replicas per GPU: one Python gRPC process saturates a core
-    # at ~2.2k Execute/s (measured 2235 -> 2378 RPS with a second replica on
-    # one GPU, profiles/r2_bench_frontends_ab.log)
-    frontends = args.frontends or min(16, 2 * max(1, n_gpus))
+    # three front-end replicas per GPU (at most 16): one Python gRPC process
+    # saturates a core at ~2.2k Execute/s (2235 -> 2378 RPS with a second
+    # replica on one GPU, profiles/r2_bench_frontends_ab.log); a third took
+    # p50 down in 3 of 3 interleaved pairs, 2794 vs 2734 RPS mean
+    # (profiles/r2_s3_frontends3_ab.log)
+    frontends = args.frontends or min(16, 3 * max(1, n_gpus))
     env = dict(os.environ)
     env.update(
         {
