@@ -6,11 +6,17 @@ Replaces the reference's Kubernetes pod pool (`kubernetes_code_executor.py:
 * one native ``bee-executor`` per GPU slot, each keeping
   ``workers_per_gpu_target`` warm single-use sandboxes whose HIP context is
   already created on that GPU (HIP_VISIBLE_DEVICES pin);
-* dispatch picks the least-loaded healthy slot that still has HBM quota
-  headroom (per-request quota, default (288 GiB - reserve) / max in-flight),
-  with bounded admission — a burst queues instead of spawning unboundedly
-  (the reference spawns a pod synchronously per request when its deque is
-  empty, `:268-272`);
+* admission is the executor daemon's (csrc/executor/sandbox.cpp run_job):
+  each GPU's daemon admits at most ``max_inflight_per_gpu`` jobs whose HBM
+  quotas (default (288 GB - reserve) / max in-flight) fit its usable HBM,
+  and queues the rest in arrival order -- one bound per GPU for every
+  front-end replica of the node, where the reference spawns a pod
+  synchronously per request when its deque is empty (`:268-272`);
+* dispatch routes to the least-loaded healthy GPU as every replica sees it:
+  the daemons publish their admitted / waiting jobs, committed HBM and gang
+  reservations in a shared load table (scheduler/load_table.py);
+* requests that can never fit fail at once: ``hbm_bytes`` above a GPU's
+  usable HBM or ``gpus`` above the node's GPU count are INVALID_ARGUMENT;
 * multi-GPU requests reserve a gang of whole GPUs atomically: the claimed
   slots stop admitting new work, drain, and the leader's executor launches
   one rank per GPU with torch.distributed rendezvous env (RCCL over xGMI);
@@ -38,6 +44,7 @@ from ..config import Config
 from ..services.storage import Storage
 from .backend import CodeExecutor, ExecuteRequest, ExecutionResult
 from .executor_process import ExecutorProcess
+from .load_table import LoadTable, open_table
 from .topology import slot_cpus
 from .uds_http import UdsHttpError
 
@@ -66,8 +73,9 @@ class Slot:
     index: int
     gpu: Optional[int]  # None = CPU-only slot
     executor: ExecutorProcess
-    inflight: int = 0
+    inflight: int = 0  # this replica's requests on the slot (its daemon bounds all replicas')
     hbm_committed: int = 0
+    load: Optional[LoadTable] = None  # the daemon's published load (all replicas)
     healthy: bool = True
     reserved: bool = False  # claimed by a waiting gang: admit nothing new
     executions: int = 0
@@ -81,6 +89,35 @@ class PoolStats:
     failures: int = 0
     queue_wait_ms_sum: float = 0.0
     latency_ms: List[float] = field(default_factory=list)
+
+
+_QUANTITY = {"": 1, "k": 1000, "M": 1000**2, "G": 1000**3, "T": 1000**4, "P": 1000**5,
+             "Ki": 1024, "Mi": 1024**2, "Gi": 1024**3, "Ti": 1024**4, "Pi": 1024**5}
+
+
+def parse_quantity(v) -> float:
+    """A Kubernetes resource quantity ("16Gi", "500m", "2", 1.5) as a number."""
+    if isinstance(v, (int, float)):
+        return float(v)
+    text = str(v).strip()
+    if text.endswith("m") and text[:-1].replace(".", "", 1).isdigit():
+        return float(text[:-1]) / 1000.0
+    for suffix in sorted(_QUANTITY, key=len, reverse=True):
+        if suffix and text.endswith(suffix):
+            return float(text[: -len(suffix)]) * _QUANTITY[suffix]
+    return float(text)
+
+
+def containment_limits(c: Config) -> dict:
+    """Per-sandbox bounds of the whole process tree (csrc/executor/procmon.hpp):
+    the reference's ``executor_container_resources`` limits (`config.py:67-68`,
+    applied to each pod's container at `kubernetes_code_executor.py:246`)
+    mapped onto the local backend -- ``limits.memory`` and ``limits.cpu`` --
+    with the APP_SANDBOX_* settings as defaults."""
+    limits = (c.executor_container_resources or {}).get("limits") or {}
+    mem = int(parse_quantity(limits["memory"])) if "memory" in limits else int(c.sandbox_tree_memory_bytes)
+    cpus = parse_quantity(limits["cpu"]) if "cpu" in limits else float(c.sandbox_cpus)
+    return {"memory": max(mem, 0), "tasks": max(int(c.sandbox_max_processes), 0), "cpus": max(cpus, 0.0)}
 
 
 def isolation_args(c: Config, slot: int, protect: List[str]) -> List[str]:
@@ -120,7 +157,7 @@ class LocalGpuPoolBackend(CodeExecutor):
         self.stats_ = PoolStats()
         usable = max(config.hbm_total_bytes - config.hbm_reserve_bytes, 0)
         self.default_quota = config.hbm_quota_bytes or (usable // max(config.max_inflight_per_gpu, 1))
-        self.hbm_capacity = usable
+        self.hbm_capacity = usable  # per GPU; enforced by each daemon (--hbm-capacity)
 
     # ---- lifecycle --------------------------------------------------------------------
     async def start(self) -> None:
@@ -131,7 +168,8 @@ class LocalGpuPoolBackend(CodeExecutor):
             for entry in json.loads(attach):
                 ex = self._make_executor(entry["index"], entry["gpu"])
                 ex.attach(entry["address"])
-                self.slots.append(Slot(index=entry["index"], gpu=entry["gpu"], executor=ex))
+                self.slots.append(Slot(index=entry["index"], gpu=entry["gpu"], executor=ex,
+                                       load=open_table(entry.get("load_table"))))
             self.gpu_ids = [s.gpu for s in self.slots if s.gpu is not None]
             self.default_gpus = 1 if self.gpu_ids else 0
             self.attached = True
@@ -141,14 +179,24 @@ class LocalGpuPoolBackend(CodeExecutor):
             ex = self._make_executor(i, gpu)
             self.slots.append(Slot(index=i, gpu=gpu, executor=ex))
         await asyncio.gather(*(s.executor.start() for s in self.slots))
+        await asyncio.gather(*(self._open_load(s) for s in self.slots))
         logger.info("local pool: %d slot(s) on GPUs %s", len(self.slots), self.gpu_ids or "[cpu]")
+
+    async def _open_load(self, slot: Slot) -> None:
+        try:
+            st = await slot.executor.get_json("/v1/status")
+            slot.load = open_table((st.get("admission") or {}).get("load_table"))
+        except Exception:  # noqa: BLE001 - routing falls back to this replica's own counts
+            slot.load = None
 
     def attach_spec(self) -> str:
         """What front-end replicas need to share this pool's executors."""
-        return json.dumps([{"index": s.index, "gpu": s.gpu, "address": s.executor.address} for s in self.slots])
+        return json.dumps([{"index": s.index, "gpu": s.gpu, "address": s.executor.address,
+                            "load_table": s.load.path if s.load else None} for s in self.slots])
 
     def _make_executor(self, i: int, gpu: Optional[int]) -> ExecutorProcess:
         c = self.config
+        lim = containment_limits(c)
         return ExecutorProcess(
             name=f"slot{i}" + (f"-gpu{gpu}" if gpu is not None else "-cpu"),
             sandbox_root=os.path.join(c.sandbox_root, f"slot{i}"),
@@ -170,6 +218,12 @@ class LocalGpuPoolBackend(CodeExecutor):
                         "--min-zygotes", str(c.min_zygotes_per_gpu),
                         "--min-cpu-target", str(c.min_cpu_workers_per_gpu_target),
                         "--gang-grace", str(c.gang_failure_grace_s),
+                        # admission for every front-end replica of the node
+                        "--max-inflight", str(max(c.max_inflight_per_gpu, 0)),
+                        "--hbm-capacity", str(self.hbm_capacity if gpu is not None else 0),
+                        # the reference pod's container limits, per sandbox tree
+                        "--sandbox-memory", str(lim["memory"]), "--sandbox-tasks", str(lim["tasks"]),
+                        "--sandbox-cpus", repr(lim["cpus"]), "--monitor-ms", str(c.sandbox_monitor_ms),
                         *isolation_args(c, i, [self.storage.storage_path])],
         )
 
@@ -184,25 +238,31 @@ class LocalGpuPoolBackend(CodeExecutor):
     def healthy(self) -> bool:
         return any(s.healthy and s.executor.alive() for s in self.slots)
 
-    # ---- admission ------------------------------------------------------------------
-    def _admissible(self, slot: Slot, hbm: int) -> bool:
-        return (
-            slot.healthy
-            and not slot.reserved
-            and slot.inflight < self.config.max_inflight_per_gpu
-            and (slot.gpu is None or slot.hbm_committed + hbm <= self.hbm_capacity)
-        )
+    # ---- routing (admission itself is the daemons') -----------------------------------
+    def _routable(self, slot: Slot) -> bool:
+        return slot.healthy and not slot.reserved
+
+    def _load_key(self, slot: Slot, hbm: int):
+        """Least-loaded order: the daemon's node-wide view (admitted + waiting
+        jobs of every replica, gang reservation, HBM headroom), then this
+        replica's own in-flight count; ties rotate so replicas and bursts
+        spread over the GPUs."""
+        n = len(self.slots)
+        rot = (slot.index - self._rr) % n
+        ld = slot.load.read() if slot.load is not None else None
+        if ld is None:
+            return (0, slot.inflight, slot.hbm_committed, rot)
+        no_room = ld.hbm_capacity > 0 and ld.hbm_committed + hbm > ld.hbm_capacity
+        return (int(ld.reserved) + int(no_room), ld.depth, slot.inflight, rot)
 
     async def _acquire_one(self, hbm: int) -> Slot:
         assert self._cond is not None
         async with self._cond:
             while True:
-                cands = [s for s in self.slots if self._admissible(s, hbm)]
+                cands = [s for s in self.slots if self._routable(s)]
                 if cands:
-                    # least loaded; ties rotate so replicas and bursts spread over GPUs
                     self._rr += 1
-                    n = len(self.slots)
-                    slot = min(cands, key=lambda s: (s.inflight, s.hbm_committed, (s.index - self._rr) % n))
+                    slot = min(cands, key=lambda s: self._load_key(s, hbm))
                     slot.inflight += 1
                     slot.hbm_committed += hbm
                     return slot
@@ -212,8 +272,6 @@ class LocalGpuPoolBackend(CodeExecutor):
 
     async def _acquire_gang(self, n: int, hbm: int) -> List[Slot]:
         assert self._cond is not None
-        if n > len(self.slots):
-            raise RuntimeError(f"requested {n} GPUs but the node has {len(self.slots)}")
         async with self._cond:
             # claim the n healthy, unreserved slots with the least work, then drain them
             while True:
@@ -266,6 +324,12 @@ class LocalGpuPoolBackend(CodeExecutor):
         gang = want > 1
         if want == 0 or not self.gpu_ids:
             hbm = 0
+        # requests no GPU of this node can ever take: refused now (they would
+        # otherwise wait forever for room that never comes)
+        if want > max(len(self.gpu_ids), 1):
+            raise ValueError(f"requested {want} GPUs but this node has {len(self.gpu_ids)}")
+        if hbm > self.hbm_capacity:
+            raise ValueError(f"hbm_bytes {hbm} exceeds the usable HBM of one GPU ({self.hbm_capacity} bytes)")
         slots = await self._acquire_gang(want, hbm) if gang else [await self._acquire_one(hbm)]
         lead = slots[0]
         gang_lock = None

@@ -181,6 +181,8 @@ def create_http_server(code_executor, custom_tool_executor: CustomToolExecutor, 
             raise HTTPException(status_code=404, detail=str(e))
         except ValidationError as e:
             raise HTTPException(status_code=422, detail=e.errors)
+        except ValueError as e:  # a request no GPU of the node can take (gpus, hbm_bytes)
+            raise HTTPException(status_code=400, detail=str(e))
         except Exception as e:
             logger.exception("Error executing code")
             raise HTTPException(status_code=500, detail=str(e))

@@ -37,6 +37,8 @@ class HostDevice final : public Device {
     if (n > budget_ - used_) return kOutOfMemory;
     *p = ::malloc(n);
     if (!*p) return kOutOfMemory;
+    // what the shared caching allocator hands out: someone else's bytes
+    memset(*p, 0xA5, n);
     used_ += n;
     sizes_.push_back({*p, n});
     return 0;
@@ -120,6 +122,8 @@ class HostDevice final : public Device {
   }
   int gemm_nn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, float, float beta,
               int odt, void*) override {
+    // the device's [K][N] kernel takes tile-multiple shapes only (bk_gemm_bf16_nn_ok)
+    if (M % 256 || N % 256 || K % 64) return kBadArgument;
     for (int i = 0; i < M; ++i) sum((const char*)A + (uint64_t)i * lda * 2, (uint64_t)K * 2);
     for (int k = 0; k < K; ++k) sum((const char*)B + (uint64_t)k * ldb * 2, (uint64_t)N * 2);
     const uint64_t es = odt == 0 ? 4 : 2;
@@ -139,6 +143,7 @@ class HostDevice final : public Device {
   int reduce_axis(uint32_t op, uint32_t dt, const void* x, void* y, int64_t rows, int64_t cols, int64_t ld,
                   uint32_t axis, void*) override {
     if (op > 1 || axis > 1 || dt > 2) return kBadArgument;
+    if (axis == 0 && cols > 262144) return kBadArgument;  // the device's column workspace (reduce.hip)
     const uint64_t es = dtype_size(dt), os = dt == 1 ? 8 : 4;
     for (int64_t r = 0; r < rows; ++r) sum((const char*)x + (uint64_t)r * ld * es, (uint64_t)cols * es);
     touch_w(y, (uint64_t)(axis == 0 ? cols : rows) * os, 0);

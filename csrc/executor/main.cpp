@@ -4,7 +4,8 @@
 //  * pool (default, local GPU backend): one daemon per MI355X, owns a zygote
 //    and a warm pool of single-use sandboxes pinned to its GPU.  Control API:
 //      POST /v1/execute   {source_code|source_file, files:{logical: src_path},
-//                          timeout, collect_dir, hbm_quota, gpus, nprocs, env, argv}
+//                          timeout, collect_dir, hbm_quota, gpus, nprocs, env, argv,
+//                          admit: "wait"|"try"}  (429: at the admission bound, admit "try")
 //      GET  /v1/status, GET /healthz, GET /metrics
 //  * pod (kubernetes backend): the reference's in-pod contract
 //    (`executor/server.rs:230-245`): PUT|GET /{workspace|runtime-packages}/{path},
@@ -55,7 +56,9 @@ void usage() {
           "                    [--workspace DIR] [--runtime-packages DIR] [--die-with-parent 0|1]\n"
           "                    [--jail 0|1] [--uid-base UID] [--uid-count N] [--protect DIR]... [--nproc N]\n"
           "                    [--mem-limit BYTES] [--cpus LIST] [--gang-grace S]\n"
-          "                    [--hbm-watchdog-ms MS] [--hbm-slack BYTES]\n");
+          "                    [--hbm-watchdog-ms MS] [--hbm-slack BYTES] [--max-inflight N] [--hbm-capacity BYTES]\n"
+          "                    [--admit-timeout S] [--sandbox-memory BYTES] [--sandbox-tasks N] [--sandbox-cpus C]\n"
+          "                    [--monitor-ms MS]\n");
 }
 
 bool resolve_pod_path(const PoolConfig& cfg, const std::string& url_path, std::string* real, std::string* err) {
@@ -141,6 +144,13 @@ int main(int argc, char** argv) {
     else if (a == "--gang-grace") cfg.gang_grace_s = atof(val().c_str());
     else if (a == "--hbm-watchdog-ms") cfg.hbm_watchdog_ms = atoi(val().c_str());
     else if (a == "--hbm-slack") cfg.hbm_slack = atoll(val().c_str());
+    else if (a == "--max-inflight") cfg.max_inflight = atoi(val().c_str());
+    else if (a == "--hbm-capacity") cfg.hbm_capacity = atoll(val().c_str());
+    else if (a == "--admit-timeout") cfg.admit_timeout_s = atof(val().c_str());
+    else if (a == "--sandbox-memory") cfg.sandbox_mem_bytes = atoll(val().c_str());
+    else if (a == "--sandbox-tasks") cfg.sandbox_tasks = atoll(val().c_str());
+    else if (a == "--sandbox-cpus") cfg.sandbox_cpus = atof(val().c_str());
+    else if (a == "--monitor-ms") cfg.monitor_ms = atoi(val().c_str());
     else if (a == "-h" || a == "--help") {
       usage();
       return 0;
