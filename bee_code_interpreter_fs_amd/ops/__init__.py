@@ -33,6 +33,7 @@ from .array import (  # noqa: F401
     is_initialized,
     log,
     matmul,
+    max_abs_diff,
     maximum,
     mean,
     memory_stats,

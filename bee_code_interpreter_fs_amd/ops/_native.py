@@ -100,6 +100,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "bk_reduce": ([c_int, c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp], c_int),
         "bk_rand_reduce": ([c_int, c_int, c_i64, c_u64, c_u64, c_d, c_d, c_vp, c_vp, c_vp], c_int),
         "bk_reduce_axis_workspace_bytes": ([], c_i64),
+        "bk_reduce_workspace_init": ([c_vp, c_vp], c_int),
+        "bk_reduce_axis_workspace_init": ([c_vp, c_vp], c_int),
         "bk_reduce_axis": ([c_int, c_int, c_vp, c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp], c_int),
         "bk_gemm_bf16_fast_ok": ([c_int, c_int, c_int, c_int, c_int], c_int),
         "bk_gemm_bf16_tn": (

@@ -35,7 +35,7 @@ _UNARY = {
     "sin": 7, "cos": 8, "tanh": 9, "sigmoid": 10, "copy": 11,
 }
 _BINARY = {"add": 0, "subtract": 1, "multiply": 2, "divide": 3, "maximum": 4, "minimum": 5, "power": 6}
-_REDUCE = {"sum": 0, "square_sum": 1, "abs_sum": 2, "max": 3, "min": 4, "dot": 5}
+_REDUCE = {"sum": 0, "square_sum": 1, "abs_sum": 2, "max": 3, "min": 4, "dot": 5, "max_abs_diff": 6}
 _SUPPORTED = ("float32", "float64", "bfloat16")
 _NP_DTYPES = {"float32": np.float32, "float64": np.float64}
 
@@ -500,6 +500,15 @@ def dot(a, b):
     if a.shape != b.shape or a.dtype != b.dtype:
         raise ValueError("dot: 1-D operands must match in shape and dtype")
     return _reduce("dot", a, b)
+
+
+def max_abs_diff(a, b) -> np.float64:
+    """max(|a - b|) in one pass (no a - b array): e.g. a result against its
+    reference.  Same shape and dtype."""
+    a, b = _as_operand(a)._materialize(), _as_operand(b)._materialize()
+    if a.shape != b.shape or a.dtype != b.dtype:
+        raise ValueError("max_abs_diff: operands must match in shape and dtype")
+    return _reduce("max_abs_diff", a, b)
 
 
 def amax(x): return _reduce("max", _as_operand(x)._materialize())

@@ -47,6 +47,7 @@ class NativeDriver:
         check(self.lib.bk_init(int(device)), "bk_init")
         self.device = device
         self.ws = self.malloc(self.lib.bk_reduce_workspace_bytes())
+        check(self.lib.bk_reduce_workspace_init(_vp(self.ws), self.stream), "bk_reduce_workspace_init")
         self.scalar = self.malloc(256)
 
     def malloc(self, nbytes: int) -> int:
@@ -110,6 +111,7 @@ class NativeDriver:
     def reduce_axis(self, op: int, dt: int, x: int, y: int, rows: int, cols: int, ld: int, axis: int) -> None:
         if not self.axis_ws:
             self.axis_ws = self.malloc(self.lib.bk_reduce_axis_workspace_bytes())
+            check(self.lib.bk_reduce_axis_workspace_init(_vp(self.axis_ws), self.stream), "bk_reduce_axis_workspace_init")
         check(self.lib.bk_reduce_axis(op, dt, _vp(x), rows, cols, ld, axis, _vp(y), _vp(self.axis_ws), self.stream),
               "bk_reduce_axis")
 

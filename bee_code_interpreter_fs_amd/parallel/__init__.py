@@ -28,9 +28,12 @@ XGMI_LINKS_PER_GPU = 7
 XGMI_LINK_GBPS = 153.0  # per direction, per link
 
 
-def rank_env(rank: int, world: int, gpus: List[int], master_port: int) -> Dict[str, str]:
-    """Environment of gang rank ``rank`` (mirrors what the executor sets)."""
-    return {
+def rank_env(rank: int, world: int, gpus: List[int], master_port: int, rdzv: Optional[str] = None) -> Dict[str, str]:
+    """Environment of gang rank ``rank`` (mirrors what the executor sets,
+    csrc/executor/sandbox.cpp run_job): ``BEE_GANG_RDZV`` is the FileStore in
+    the gang's private directory that ``init_process_group()`` uses by
+    default (runtime/sandbox_patches.py); RCCL's bootstrap stays on loopback."""
+    env = {
         "RANK": str(rank),
         "LOCAL_RANK": str(rank),
         "WORLD_SIZE": str(world),
@@ -38,7 +41,11 @@ def rank_env(rank: int, world: int, gpus: List[int], master_port: int) -> Dict[s
         "MASTER_ADDR": "127.0.0.1",
         "MASTER_PORT": str(master_port),
         "HIP_VISIBLE_DEVICES": ",".join(str(g) for g in gpus),
+        "NCCL_SOCKET_IFNAME": "lo",
     }
+    if rdzv:
+        env["BEE_GANG_RDZV"] = rdzv
+    return env
 
 
 def init_process_group(backend: Optional[str] = None):
@@ -56,14 +63,22 @@ def init_process_group(backend: Optional[str] = None):
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl":
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    dist.init_process_group(backend, rank=rank, world_size=world)
+    rdzv = os.environ.get("BEE_GANG_RDZV")
+    if rdzv:
+        dist.init_process_group(backend, init_method=rdzv, rank=rank, world_size=world)
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     return rank, world
 
 
 def busbw_budget_gbps(world: int) -> float:
-    """Upper bound of ring all-reduce bus bandwidth per GPU if RCCL spreads
-    its channels over all xGMI links of a fully connected node."""
-    return XGMI_LINKS_PER_GPU * XGMI_LINK_GBPS if world > 1 else float("inf")
+    """Upper bound of all-reduce bus bandwidth per GPU: the node is fully
+    connected (one xGMI link between every pair of its 8 GPUs), so a gang of
+    ``world`` GPUs reaches its peers over world - 1 links of ~153 GB/s each
+    (all 7 at world = 8), if RCCL spreads its channels over all of them."""
+    if world <= 1:
+        return float("inf")
+    return min(world - 1, XGMI_LINKS_PER_GPU) * XGMI_LINK_GBPS
 
 
 def rccl_allreduce_sweep(

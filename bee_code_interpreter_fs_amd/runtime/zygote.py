@@ -237,7 +237,7 @@ def main() -> None:
     def send(msg: dict) -> None:
         chan.sendall((json.dumps(msg) + "\n").encode())
 
-    send({"op": "hello", "pid": os.getpid(), "preloaded": loaded, "import_ms": import_ms})
+    send({"op": "hello", "pid": os.getpid(), "preloaded": loaded, "import_ms": import_ms, "net_layer": jail.net_state()})
 
     from . import worker
 

@@ -59,7 +59,10 @@ class HipDevice final : public broker::Device {
     int (*gemm_nn)(const void*, const void*, void*, int, int, int, int, int, int, float, float, int, hipStream_t);
     int (*transpose)(int, int, const void*, void*, int, int, int, int, hipStream_t);
     int (*preload)(hipStream_t);
+    int (*reserve)(int64_t);
     int64_t (*axis_ws)();
+    int (*ws_init)(void*, hipStream_t);       // zero a fresh workspace's completion tickets
+    int (*axis_ws_init)(void*, hipStream_t);
     int (*reduce_axis)(int, int, const void*, int64_t, int64_t, int64_t, int, void*, void*, hipStream_t);
   } bk{};
 
@@ -159,7 +162,12 @@ class HipDevice final : public broker::Device {
       return false;
     }
     sym(lib_, "bk_preload", &bk.preload);
+    sym(lib_, "bk_reserve", &bk.reserve);
     sym(lib_, "bk_reduce_axis_workspace_bytes", &bk.axis_ws);
+    if (!sym(lib_, "bk_reduce_workspace_init", &bk.ws_init) || !sym(lib_, "bk_reduce_axis_workspace_init", &bk.axis_ws_init)) {
+      *err = "libbeekern.so has no reduction workspace init (stale build)";
+      return false;
+    }
     sym(lib_, "bk_reduce_axis", &bk.reduce_axis);
     sym(lib_, "bk_gemm_bf16_nn", &bk.gemm_nn);
     return true;
@@ -182,6 +190,16 @@ class HipDevice final : public broker::Device {
       return false;
     }
     bk.set_quota(0);  // quotas are enforced per sandbox by the sessions
+    if (bk.reserve) {
+      // large blocks come from segments from now on; the first one now, so a
+      // freshly started broker serves its first requests without hipMallocs
+      // (BEE_BROKER_RESERVE_BYTES, default 8 GiB of the GPU's 288)
+      const char* rb = getenv("BEE_BROKER_RESERVE_BYTES");
+      const int64_t bytes = rb && *rb ? strtoll(rb, nullptr, 10) : (8ll << 30);
+      const double tr = mono_ms();
+      if (bk.reserve(bytes) != 0) BEE_WARN("broker: reserving %lld bytes failed: %s", (long long)bytes, bk.last_error());
+      else BEE_INFO("kernel broker: %lld MiB reserved in %.0f ms", (long long)(bytes >> 20), mono_ms() - tr);
+    }
     if (bk.preload) {  // every kernel module now, not on a sandbox's first request
       const double tp = mono_ms();
       const int rc = bk.preload(nullptr);
@@ -211,6 +229,7 @@ class HipDevice final : public broker::Device {
     hipSetDevice(0);
     hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
     bk.malloc_(&c->ws, bk.reduce_ws());
+    bk.ws_init(c->ws, c->s);  // (ordered before every reduction on this stream)
     bk.malloc_(&c->scalar, 256);
     void* page = nullptr;
     if (hipHostMalloc(&page, 64, hipHostMallocCoherent) == hipSuccess) c->slot = (double*)page;
@@ -313,7 +332,10 @@ class HipDevice final : public broker::Device {
                   uint32_t axis, void* s) override {
     Ctx* c = (Ctx*)s;
     if (!bk.reduce_axis || !bk.axis_ws) return broker::kBadArgument;
-    if (!c->axis_ws && bk.malloc_(&c->axis_ws, bk.axis_ws()) != 0) return broker::kOutOfMemory;
+    if (!c->axis_ws) {
+      if (bk.malloc_(&c->axis_ws, bk.axis_ws()) != 0) return broker::kOutOfMemory;
+      bk.axis_ws_init(c->axis_ws, c->s);
+    }
     return bk.reduce_axis((int)op, (int)dt, x, rows, cols, ld, (int)axis, y, c->axis_ws, c->s);
   }
   const char* last_error() override { return bk.last_error ? bk.last_error() : ""; }

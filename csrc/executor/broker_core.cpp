@@ -305,7 +305,7 @@ int32_t Session::dispatch(uint32_t op, const char* payload, uint64_t len, std::v
       const uint64_t a = r.get<uint64_t>(), bh = r.get<uint64_t>();
       const int64_t n = r.get<int64_t>();
       if (!r.ok) return kProtocol;
-      const bool two = rop == 5;  // dot reads b
+      const bool two = rop == 5 || rop == 6;  // dot and max|a-b| read b
       uint64_t need;
       Buf *ba = lookup(a), *bb = two ? lookup(bh) : nullptr;
       if (n < 0 || !dtype_size(dt) || !mul_ok((uint64_t)n, dtype_size(dt), &need) || !ba || need > ba->size ||

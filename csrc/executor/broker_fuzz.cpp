@@ -98,7 +98,7 @@ class HostDevice final : public Device {
     return 0;
   }
   int reduce(uint32_t op, uint32_t dt, const void* a, const void* b, int64_t n, double* out, void*) override {
-    if (op > 5 || dt > 2 || (op == 5 && !b)) return kBadArgument;
+    if (op > 6 || dt > 2 || ((op == 5 || op == 6) && !b)) return kBadArgument;
     *out = sum(a, (uint64_t)n * dtype_size(dt)) + (b ? sum(b, (uint64_t)n * dtype_size(dt)) : 0);
     return 0;
   }

@@ -145,7 +145,10 @@ int64_t vram_bytes(pid_t pid, std::set<std::string>* clients, bool* has_render) 
 
 int kill_tree(pid_t leader, int rounds) {
   if (leader <= 0) return 0;
-  // a stopped leader still adopts the orphans of what is killed below it
+  // freeze the leader's process group first (atomic for its members: a fork
+  // bomb in it stops growing); a stopped leader still adopts the orphans of
+  // what is killed below it
+  kill(-leader, SIGSTOP);
   kill(leader, SIGSTOP);
   std::set<pid_t> signalled;
   std::vector<pid_t> pids;

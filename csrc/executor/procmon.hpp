@@ -52,11 +52,12 @@ int64_t pss_anon_bytes(pid_t pid);
 // drm-total-vram, one count per DRM client); *has_render set if it holds any
 int64_t vram_bytes(pid_t pid, std::set<std::string>* clients, bool* has_render);
 
-// SIGKILL every process of the tree: the process group first (atomic for its
-// members), then whatever the walk still finds -- children before the
-// leader, so orphans re-parent to the (still living) leader and are found by
-// the next round -- until the tree is empty or `rounds` ran out.  Returns the
-// number of processes signalled.
+// SIGKILL every process of the tree: the process group is stopped first
+// (atomic for its members), then whatever the walk finds is killed --
+// children before the leader, so orphans re-parent to the (stopped, living)
+// leader and are found by the next round -- until a round finds nothing new
+// or `rounds` ran out; the group and the leader last.  Returns the number of
+// processes signalled.
 int kill_tree(pid_t leader, int rounds = 64);
 // SIGSTOP / SIGCONT the tree (CPU throttling)
 void signal_tree(pid_t leader, int sig);

@@ -560,6 +560,11 @@ BK_API int bk_gemm_bf16_fast_ok(int M, int N, int K, int lda, int ldb) {
 
 // the edge kernel: any M, N; 16-B chunks (K, ld multiples of 8); a 128-row
 // tile's byte extent within the 31-bit buffer offsets
+// the skinny kernel's 16-B loads: K, lda, ldb multiples of 8 elements
+static bool skinny_ok(const void* A, const void* Bt, int N, int K, int lda, int ldb) {
+  return aligned16(A) && aligned16(Bt) && N <= kSkinnyCols && K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0;
+}
+
 static bool edge_ok(int M, int N, int K, int lda, int ldb) {
   return M > 0 && N > 0 && K > 0 && K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
          (int64_t)BM * lda * 2 < 0x7fffffffll && (int64_t)BN * ldb * 2 < 0x7fffffffll;
@@ -575,8 +580,9 @@ static bool edge_ok(int M, int N, int K, int lda, int ldb) {
 // mode (variant 7; K % 8 == 0) when they fill the chip.
 // variant: 0 = auto, 1 = generic, 2 = 128x128, 3 = 256x256 (4-wave or 8-wave
 // by K), 4 = 256x256 8-wave, 5 = 256x256 4-wave, 6 = 128x128 edge, 7 = 256x256
-// 4-wave edge (benchmarks, tests).
-static int auto_variant(bool ok256, bool ok128, bool okedge, bool ok256e, int M, int N) {
+// 4-wave edge, 8 = skinny (N <= 16: a matrix-vector product) (benchmarks, tests).
+static int auto_variant(bool ok256, bool ok128, bool okedge, bool ok256e, bool okskinny, int M, int N) {
+  if (okskinny) return 8;  // GEMV-shaped (N <= 16): read A once, no mostly-empty tiles
   const int64_t tiles256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
   if (ok256 && (M / 256) * (N / 256) >= 128) return 3;
   if (ok128) return 2;
@@ -593,12 +599,21 @@ BK_API int bk_gemm_bf16_tn_variant(const void* A, const void* Bt, void* C, int M
   const bool ok256 = al && aligned16(C) && gemm256_ok(M, N, K, lda, ldb, ldc, out_dtype == kBF16);
   const bool okedge = al && edge_ok(M, N, K, lda, ldb);
   const bool ok256e = al && gemm256_edge_ok(M, N, K, lda, ldb);
-  if (variant == 0) variant = auto_variant(ok256, ok128, okedge, ok256e, M, N);
+  const bool okskinny = skinny_ok(A, Bt, N, K, lda, ldb);
+  if (variant == 0) variant = auto_variant(ok256, ok128, okedge, ok256e, okskinny, M, N);
   if ((variant >= 3 && variant <= 5 && !ok256) || (variant == 2 && !ok128) || (variant == 6 && !okedge) ||
-      (variant == 7 && !ok256e) || variant < 1 || variant > 7)
+      (variant == 7 && !ok256e) || (variant == 8 && !okskinny) || variant < 1 || variant > 8)
     return kBadArgument;
   const bool bf = out_dtype == kBF16;
-  if (variant == 7) {
+  if (variant == 8) {
+    const unsigned g = (unsigned)((M + 4 * kSkinnyRows - 1) / (4 * kSkinnyRows));
+    if (bf)
+      gemm_bf16_tn_skinny<true><<<g, 256, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N, K, lda, ldb,
+                                                       ldc, alpha, beta);
+    else
+      gemm_bf16_tn_skinny<false><<<g, 256, 0, stream>>>((const uint16_t*)A, (const uint16_t*)Bt, C, M, N, K, lda, ldb,
+                                                        ldc, alpha, beta);
+  } else if (variant == 7) {
     // a remainder of <= 64 rows / columns past the 256-multiples would cost a
     // whole extra wave of mostly-empty 256^2 tiles (4095 x 4097: 272 tiles on
     // 256 CUs); it goes to the 128^2 edge kernel as a strip after the main
@@ -667,7 +682,8 @@ BK_API int bk_gemm_bf16_pick(const void* A, const void* Bt, const void* C, int M
   const bool al = aligned16(A) && aligned16(Bt);
   const bool ok128 = al && bk_gemm_bf16_fast_ok(M, N, K, lda, ldb);
   const bool ok256 = al && aligned16(C) && gemm256_ok(M, N, K, lda, ldb, ldc, out_dtype == kBF16);
-  return auto_variant(ok256, ok128, al && edge_ok(M, N, K, lda, ldb), al && gemm256_edge_ok(M, N, K, lda, ldb), M, N);
+  return auto_variant(ok256, ok128, al && edge_ok(M, N, K, lda, ldb), al && gemm256_edge_ok(M, N, K, lda, ldb),
+                      skinny_ok(A, Bt, N, K, lda, ldb), M, N);
 }
 
 // C = alpha * A . B + beta * C with B stored [K][N] (leading dimension ldb):

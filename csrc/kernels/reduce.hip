@@ -3,17 +3,24 @@
 // (`examples/benchmark-numpy.py:21`) is kRedSquareSum on f64 — one HBM pass
 // (800 MB read for 1e8 f64) instead of numpy's write-then-read of x².
 //
-// Stage 1: <= 32 blocks per CU, each lane streams 16-B vectors (16 in flight,
-// non-temporal past the Infinity Cache),
-// accumulates in f64, wave-reduces over 64 lanes (DPP) -> LDS -> one partial
-// per block.  Stage 2: one block folds the partials in a fixed order.  No
-// float atomics, so results are bitwise reproducible run to run.
+// One launch: <= 32 blocks per CU, each lane streams 16-B vectors (16 in
+// flight, non-temporal past the Infinity Cache), accumulates in f64,
+// wave-reduces over 64 lanes (DPP) -> LDS -> one partial per block; the block
+// that takes the last completion ticket folds every partial in a fixed order
+// (index order, the same tree whichever block is last).  No float atomics,
+// so results are bitwise reproducible run to run.  (A second single-block
+// launch used to do the fold: under concurrent sandboxes it queued behind
+// other tenants' GEMMs holding every CU -- 25 us mean for a 1.8 us kernel,
+// profiles/r2_s3_final_served_path_kernels.csv.)
 #include "bk_common.hpp"
 #include "bk_philox.hpp"
 
 namespace bk {
 
-enum ReduceOp : int { kRedSum = 0, kRedSquareSum, kRedAbsSum, kRedMax, kRedMin, kRedDot, kRedCount };
+// kRedMaxAbsDiff: max |a - b| (two operands, like kRedDot) -- one pass where
+// subtract + abs + max would be three (e.g. a row check against a reference)
+enum ReduceOp : int { kRedSum = 0, kRedSquareSum, kRedAbsSum, kRedMax, kRedMin, kRedDot, kRedMaxAbsDiff, kRedCount };
+template <int OP> constexpr bool kTwoOperands = OP == kRedDot || OP == kRedMaxAbsDiff;
 
 constexpr int kRedBlock = 256;
 // stage-1 grid cap, and the workspace length: 32 blocks per CU with 16 loads
@@ -31,6 +38,7 @@ template <> __device__ __forceinline__ double to_f64<uint16_t>(uint16_t v) { ret
 
 template <int OP> __device__ __forceinline__ double red_init() {
   if constexpr (OP == kRedMax) return -INFINITY;
+  else if constexpr (OP == kRedMaxAbsDiff) return 0.0;
   else if constexpr (OP == kRedMin) return INFINITY;
   else return 0.0;
 }
@@ -38,10 +46,11 @@ template <int OP> __device__ __forceinline__ double red_map(double a, double b) 
   if constexpr (OP == kRedSquareSum) return a * a;
   else if constexpr (OP == kRedAbsSum) return fabs(a);
   else if constexpr (OP == kRedDot) return a * b;
+  else if constexpr (OP == kRedMaxAbsDiff) return fabs(a - b);
   else return a;
 }
 template <int OP> __device__ __forceinline__ double red_combine(double x, double y) {
-  if constexpr (OP == kRedMax) return fmax(x, y);
+  if constexpr (OP == kRedMax || OP == kRedMaxAbsDiff) return fmax(x, y);
   else if constexpr (OP == kRedMin) return fmin(x, y);
   else return x + y;
 }
@@ -69,9 +78,57 @@ template <int OP> __device__ __forceinline__ double block_reduce(double v) {
 
 template <typename T> struct alignas(16) V16 { T v[16 / sizeof(T)]; };
 
+// ---- single-launch completion ------------------------------------------------
+// Every block publishes its partial, then takes a ticket; the block holding
+// the last ticket folds the partials and re-arms the ticket for the next
+// launch on this workspace.  Tickets start at zero (bk_reduce_workspace_init).
+//
+// Blocks sit on different XCDs, each with its own L2.  Partials are written
+// and read with agent-scope (sc1) accesses, which are coherent across XCDs;
+// a store is complete (vmcnt: GFX9 counts stores there) before its block's
+// ticket.  No release/acquire fences: at agent scope those write back and
+// invalidate the whole L2 (buffer_wbl2 / buffer_inv), per block -- what the
+// first version of this did cost every reduction ~1 ms under concurrent
+// sandboxes.
+__device__ __forceinline__ void publish(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool take_last_ticket(unsigned* ticket, unsigned count) {
+  __shared__ bool last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == count - 1;
+  }
+  __syncthreads();
+  return last;
+}
+__device__ __forceinline__ double load_agent(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void rearm(unsigned* ticket) {
+  __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the fold of `count` partials into *out by the last block
+template <int OP>
+__device__ __forceinline__ void finish(double v, double* partials, unsigned* ticket, double* out) {
+  if (threadIdx.x == 0) publish(partials + blockIdx.x, v);
+  if (!take_last_ticket(ticket, gridDim.x)) return;
+  double r = red_init<OP>();
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += kRedBlock) r = red_combine<OP>(r, load_agent(partials + i));
+  r = block_reduce<OP>(r);
+  if (threadIdx.x == 0) {
+    *out = r;
+    rearm(ticket);
+  }
+}
+
 template <typename T, int OP, bool NT>
-__global__ __launch_bounds__(kRedBlock) void reduce_stage1(const T* __restrict__ a, const T* __restrict__ b, int64_t n,
-                                                          double* __restrict__ partials) {
+__global__ __launch_bounds__(kRedBlock) void reduce_1pass(const T* __restrict__ a, const T* __restrict__ b, int64_t n,
+                                                         double* __restrict__ partials, unsigned* __restrict__ ticket,
+                                                         double* __restrict__ out) {
   using V = V16<T>;
   constexpr int N = 16 / sizeof(T);
   constexpr int U = kRedUnroll;  // 16-B loads in flight per lane
@@ -88,44 +145,34 @@ __global__ __launch_bounds__(kRedBlock) void reduce_stage1(const T* __restrict__
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       va[u] = ld16<NT>(reinterpret_cast<const V*>(a) + i + u * stride);
-      if constexpr (OP == kRedDot) vb[u] = ld16<NT>(reinterpret_cast<const V*>(b) + i + u * stride);
+      if constexpr (kTwoOperands<OP>) vb[u] = ld16<NT>(reinterpret_cast<const V*>(b) + i + u * stride);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < N; ++j) {
-        const double bj = (OP == kRedDot) ? to_f64<T>(vb[u].v[j]) : 0.0;
+        const double bj = kTwoOperands<OP> ? to_f64<T>(vb[u].v[j]) : 0.0;
         acc[u] = red_combine<OP>(acc[u], red_map<OP>(to_f64<T>(va[u].v[j]), bj));
       }
   }
   for (; i < nvec; i += stride) {
     V va = reinterpret_cast<const V*>(a)[i];
     V vb;
-    if constexpr (OP == kRedDot) vb = reinterpret_cast<const V*>(b)[i];
+    if constexpr (kTwoOperands<OP>) vb = reinterpret_cast<const V*>(b)[i];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      const double bj = (OP == kRedDot) ? to_f64<T>(vb.v[j]) : 0.0;
+      const double bj = kTwoOperands<OP> ? to_f64<T>(vb.v[j]) : 0.0;
       acc[0] = red_combine<OP>(acc[0], red_map<OP>(to_f64<T>(va.v[j]), bj));
     }
   }
   for (int64_t k = nvec * N + tid; k < n; k += stride) {
-    const double bk_ = (OP == kRedDot) ? to_f64<T>(b[k]) : 0.0;
+    const double bk_ = kTwoOperands<OP> ? to_f64<T>(b[k]) : 0.0;
     acc[0] = red_combine<OP>(acc[0], red_map<OP>(to_f64<T>(a[k]), bk_));
   }
   double v = acc[0];
 #pragma unroll
   for (int u = 1; u < U; ++u) v = red_combine<OP>(v, acc[u]);
-  v = block_reduce<OP>(v);
-  if (threadIdx.x == 0) partials[blockIdx.x] = v;
-}
-
-template <int OP>
-__global__ __launch_bounds__(kRedBlock) void reduce_stage2(const double* __restrict__ partials, int count,
-                                                          double* __restrict__ out) {
-  double v = red_init<OP>();
-  for (int i = threadIdx.x; i < count; i += kRedBlock) v = red_combine<OP>(v, partials[i]);
-  v = block_reduce<OP>(v);
-  if (threadIdx.x == 0) *out = v;
+  finish<OP>(block_reduce<OP>(v), partials, ticket, out);
 }
 
 // ---- fused RNG -> reduce -------------------------------------------------------
@@ -144,7 +191,8 @@ __device__ __forceinline__ double rr_map(double v) {
 
 template <int OP>
 __global__ __launch_bounds__(kRedBlock) void rand_reduce_f64(int64_t n, uint32_t k0, uint32_t k1, uint64_t offset,
-                                                             double lo, double span, double* __restrict__ partials) {
+                                                             double lo, double span, double* __restrict__ partials,
+                                                             unsigned* __restrict__ ticket, double* __restrict__ out) {
   const int64_t pairs = (n + 1) / 2, full = n / 2;  // `full`: pairs whose both values are in range
   const int64_t stride = (int64_t)gridDim.x * kRedBlock;
   double acc0 = 0.0, acc1 = 0.0;
@@ -162,13 +210,13 @@ __global__ __launch_bounds__(kRedBlock) void rand_reduce_f64(int64_t n, uint32_t
     acc0 += rr_map<OP>(lo + span * u53(r0.x, r0.y));
     if (2 * p + 1 < n) acc0 += rr_map<OP>(lo + span * u53(r0.z, r0.w));
   }
-  const double v = block_reduce<OP>(acc0 + acc1);
-  if (threadIdx.x == 0) partials[blockIdx.x] = v;
+  finish<OP>(block_reduce<OP>(acc0 + acc1), partials, ticket, out);
 }
 
 template <int OP>
 __global__ __launch_bounds__(kRedBlock) void rand_reduce_f32(int64_t n, uint32_t k0, uint32_t k1, uint64_t offset,
-                                                             float lo, float span, double* __restrict__ partials) {
+                                                             float lo, float span, double* __restrict__ partials,
+                                                             unsigned* __restrict__ ticket, double* __restrict__ out) {
   const int64_t quads = (n + 3) / 4;
   const int64_t stride = (int64_t)gridDim.x * kRedBlock;
   double acc = 0.0;
@@ -180,8 +228,7 @@ __global__ __launch_bounds__(kRedBlock) void rand_reduce_f32(int64_t n, uint32_t
     for (int j = 0; j < 4; ++j)
       if (4 * q + j < n) acc += rr_map<OP>((double)v[j]);
   }
-  const double v = block_reduce<OP>(acc);
-  if (threadIdx.x == 0) partials[blockIdx.x] = v;
+  finish<OP>(block_reduce<OP>(acc), partials, ticket, out);
 }
 
 template <typename T, int OP>
@@ -190,11 +237,11 @@ int launch_reduce(const void* a, const void* b, int64_t n, double* workspace, do
   int64_t lanes_needed = (n / N + 3) / 4;  // 4 vectors per lane minimum before adding blocks
   unsigned g = stream_grid(lanes_needed > 0 ? lanes_needed : 1, kRedBlock, kRedMaxBlocks / kNumCU);
   if (g > (unsigned)kRedMaxBlocks) g = kRedMaxBlocks;  // the workspace holds kRedMaxBlocks partials
-  if (stream_nt(n * (int64_t)sizeof(T) * (OP == kRedDot ? 2 : 1)))
-    reduce_stage1<T, OP, true><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace);
+  unsigned* ticket = reinterpret_cast<unsigned*>(workspace + kRedMaxBlocks);
+  if (stream_nt(n * (int64_t)sizeof(T) * (kTwoOperands<OP> ? 2 : 1)))
+    reduce_1pass<T, OP, true><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
   else
-    reduce_stage1<T, OP, false><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace);
-  reduce_stage2<OP><<<1, kRedBlock, 0, s>>>(workspace, (int)g, out);
+    reduce_1pass<T, OP, false><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
   return launch_status();
 }
 
@@ -210,32 +257,54 @@ int dispatch_reduce(int op, const void* a, const void* b, int64_t n, double* ws,
 // axis 0 (per column): a block of 256 threads owns 256 columns of one row
 // chunk -- each thread walks its column down the chunk, so every wave-row
 // load is 64 consecutive elements; the chunk partials (f64) land in the
-// workspace and a second pass folds them in chunk order (deterministic).
+// workspace and the last chunk block of each column block (completion
+// tickets, as above) folds them in chunk order (deterministic) -- one launch.
 // axis 1 (per row): one wave per row, lanes stride the row, DPP wave sum.
 constexpr int64_t kAxisWsDoubles = 1 << 18;  // 2 MiB: chunks x columns partials
+constexpr int64_t kAxisTickets = 4096;       // one per column block (<= 2048 at 262144 columns)
 
-template <typename T>
-__global__ __launch_bounds__(256) void colsum_partial(const T* __restrict__ x, int64_t rows, int64_t cols, int64_t ld,
-                                                      int64_t rows_per_chunk, double* __restrict__ part) {
+// out[col] = scale * the chunk partials of `col` folded in a fixed order: four
+// chains (chunks c, c+4, c+8, c+12) so a thread's loads are in flight together
+__device__ __forceinline__ double fold_chunks(const double* part, int chunks, int64_t cols, int64_t col) {
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  int c = 0;
+  for (; c + 15 < chunks; c += 16)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] += load_agent(part + (int64_t)(c + 4 * j + q) * cols + col);
+  for (; c < chunks; ++c) a[c & 3] += load_agent(part + (int64_t)c * cols + col);
+  return (a[0] + a[1]) + (a[2] + a[3]);
+}
+
+template <typename T, typename TO>
+__global__ __launch_bounds__(256) void colsum_1pass(const T* __restrict__ x, int64_t rows, int64_t cols, int64_t ld,
+                                                    int64_t rows_per_chunk, double* __restrict__ part,
+                                                    unsigned* __restrict__ tickets, TO* __restrict__ out, double scale) {
   const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (col >= cols) return;
-  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
-  const int64_t r1 = r0 + rows_per_chunk < rows ? r0 + rows_per_chunk : rows;
-  double a0 = 0.0, a1 = 0.0;
-  int64_t r = r0;
-  for (; r + 1 < r1; r += 2) {
-    a0 += to_f64<T>(x[r * ld + col]);
-    a1 += to_f64<T>(x[(r + 1) * ld + col]);
+  if (col < cols) {
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+    const int64_t r1 = r0 + rows_per_chunk < rows ? r0 + rows_per_chunk : rows;
+    double a0 = 0.0, a1 = 0.0;
+    int64_t r = r0;
+    for (; r + 1 < r1; r += 2) {
+      a0 += to_f64<T>(x[r * ld + col]);
+      a1 += to_f64<T>(x[(r + 1) * ld + col]);
+    }
+    if (r < r1) a0 += to_f64<T>(x[r * ld + col]);
+    publish(part + (int64_t)blockIdx.y * cols + col, a0 + a1);
   }
-  if (r < r1) a0 += to_f64<T>(x[r * ld + col]);
-  part[(int64_t)blockIdx.y * cols + col] = a0 + a1;
+  if (!take_last_ticket(tickets + blockIdx.x, gridDim.y)) return;
+  if (col < cols) out[col] = (TO)(fold_chunks(part, (int)gridDim.y, cols, col) * scale);
+  if (threadIdx.x == 0) rearm(tickets + blockIdx.x);
 }
 
 // 16-B vectors per lane (V columns), 4 row groups per block: a wave reads one
 // contiguous 1 KiB (bf16) row segment per step
-template <typename T>
-__global__ __launch_bounds__(256) void colsum_partial_v(const T* __restrict__ x, int64_t rows, int64_t cols, int64_t ld,
-                                                        int64_t rows_per_chunk, double* __restrict__ part) {
+template <typename T, typename TO>
+__global__ __launch_bounds__(256) void colsum_1pass_v(const T* __restrict__ x, int64_t rows, int64_t cols, int64_t ld,
+                                                      int64_t rows_per_chunk, double* __restrict__ part,
+                                                      unsigned* __restrict__ tickets, TO* __restrict__ out, double scale) {
   constexpr int V = 16 / sizeof(T);
   __shared__ double sacc[4][64 * V];
   const int tx = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -259,34 +328,14 @@ __global__ __launch_bounds__(256) void colsum_partial_v(const T* __restrict__ x,
   // 256 threads fold the 4 row groups of 64*V columns
   for (int c = threadIdx.x; c < 64 * V; c += 256) {
     const int64_t col = (int64_t)blockIdx.x * 64 * V + c;
-    if (col < cols) part[(int64_t)blockIdx.y * cols + col] = sacc[0][c] + sacc[1][c] + sacc[2][c] + sacc[3][c];
+    if (col < cols) publish(part + (int64_t)blockIdx.y * cols + col, sacc[0][c] + sacc[1][c] + sacc[2][c] + sacc[3][c]);
   }
-}
-
-// fold the chunk partials: 4 threads per column (strided chunks), LDS combine
-template <typename TO>
-__global__ __launch_bounds__(256) void colsum_final(const double* __restrict__ part, int chunks, int64_t cols,
-                                                    TO* __restrict__ out, double scale) {
-  __shared__ double s4[4][64];
-  const int tx = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
-  // four independent chains (chunks c, c+4, c+8, c+12): the loads of one
-  // thread are in flight together instead of one HBM latency per chunk
-  double a[4] = {0.0, 0.0, 0.0, 0.0};
-  if (col < cols) {
-    int c = g;
-    for (; c + 12 < chunks; c += 16) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) a[j] += part[(int64_t)(c + 4 * j) * cols + col];
-    }
-    // (at most three chunks left: c, c+4, c+8)
-    if (c < chunks) a[0] += part[(int64_t)c * cols + col];
-    if (c + 4 < chunks) a[1] += part[(int64_t)(c + 4) * cols + col];
-    if (c + 8 < chunks) a[2] += part[(int64_t)(c + 8) * cols + col];
+  if (!take_last_ticket(tickets + blockIdx.x, gridDim.y)) return;
+  for (int c = threadIdx.x; c < 64 * V; c += 256) {
+    const int64_t col = (int64_t)blockIdx.x * 64 * V + c;
+    if (col < cols) out[col] = (TO)(fold_chunks(part, (int)gridDim.y, cols, col) * scale);
   }
-  s4[g][tx] = (a[0] + a[1]) + (a[2] + a[3]);
-  __syncthreads();
-  if (g == 0 && col < cols) out[col] = (TO)(((s4[0][tx] + s4[1][tx]) + (s4[2][tx] + s4[3][tx])) * scale);
+  if (threadIdx.x == 0) rearm(tickets + blockIdx.x);
 }
 
 template <typename T, typename TO>
@@ -302,14 +351,46 @@ __global__ __launch_bounds__(256) void rowsum(const T* __restrict__ x, int64_t r
   if (lane == 0) out[row] = (TO)(acc * scale);
 }
 
+// 16-B vectors: a wave reads 1 KiB of its row per step (bf16: 512 columns)
+template <typename T, typename TO>
+__global__ __launch_bounds__(256) void rowsum_v(const T* __restrict__ x, int64_t rows, int64_t cols, int64_t ld,
+                                                TO* __restrict__ out, double scale) {
+  constexpr int V = 16 / sizeof(T);
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const V16<T>* p = reinterpret_cast<const V16<T>*>(x + row * ld);
+  const int64_t nv = cols / V;
+  double a0 = 0.0, a1 = 0.0;
+  int64_t c = lane;
+  for (; c + 64 < nv; c += 128) {  // two vectors in flight per lane
+    const V16<T> u = p[c], w = p[c + 64];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      a0 += to_f64<T>(u.v[j]);
+      a1 += to_f64<T>(w.v[j]);
+    }
+  }
+  if (c < nv) {
+    const V16<T> u = p[c];
+#pragma unroll
+    for (int j = 0; j < V; ++j) a0 += to_f64<T>(u.v[j]);
+  }
+  const double acc = wave_reduce<kRedSum>(a0 + a1);
+  if (lane == 0) out[row] = (TO)(acc * scale);
+}
+
 template <typename T, typename TO>
 int launch_axis(const T* x, int64_t rows, int64_t cols, int64_t ld, int axis, TO* out, double scale, double* ws,
                 hipStream_t s) {
+  constexpr int V = 16 / sizeof(T);
   if (axis == 1) {
-    rowsum<T, TO><<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(x, rows, cols, ld, out, scale);
+    if (cols % V == 0 && ld % V == 0 && ((uintptr_t)x & 15) == 0)
+      rowsum_v<T, TO><<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(x, rows, cols, ld, out, scale);
+    else
+      rowsum<T, TO><<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(x, rows, cols, ld, out, scale);
     return launch_status();
   }
-  constexpr int V = 16 / sizeof(T);
   const bool vec = cols % V == 0 && ld % V == 0 && ((uintptr_t)x & 15) == 0;
   const int64_t col_blocks = vec ? (cols + 64 * V - 1) / (64 * V) : (cols + 255) / 256;
   // enough row chunks for ~1k blocks, as far as the workspace allows; each
@@ -320,11 +401,13 @@ int launch_axis(const T* x, int64_t rows, int64_t cols, int64_t ld, int axis, TO
   if (chunks < 1) chunks = 1;
   const int64_t per = (rows + chunks - 1) / chunks;
   chunks = (rows + per - 1) / per;
+  unsigned* tickets = reinterpret_cast<unsigned*>(ws + kAxisWsDoubles);
+  if (col_blocks > kAxisTickets) return kBadArgument;
+  const dim3 grid((unsigned)col_blocks, (unsigned)chunks);
   if (vec)
-    colsum_partial_v<T><<<dim3((unsigned)col_blocks, (unsigned)chunks), 256, 0, s>>>(x, rows, cols, ld, per, ws);
+    colsum_1pass_v<T, TO><<<grid, 256, 0, s>>>(x, rows, cols, ld, per, ws, tickets, out, scale);
   else
-    colsum_partial<T><<<dim3((unsigned)col_blocks, (unsigned)chunks), 256, 0, s>>>(x, rows, cols, ld, per, ws);
-  colsum_final<TO><<<(unsigned)((cols + 63) / 64), 256, 0, s>>>(ws, (int)chunks, cols, out, scale);
+    colsum_1pass<T, TO><<<grid, 256, 0, s>>>(x, rows, cols, ld, per, ws, tickets, out, scale);
   return launch_status();
 }
 
@@ -344,27 +427,37 @@ BK_API int bk_rand_reduce(int op, int dtype, int64_t n, uint64_t seed, uint64_t 
   unsigned g = stream_grid(units > 0 ? (units + 7) / 8 : 1, kRedBlock, kRandRedMaxBlocks / kNumCU);
   if (g > (unsigned)kRandRedMaxBlocks) g = kRandRedMaxBlocks;
   double* ws = (double*)workspace;
+  unsigned* t = reinterpret_cast<unsigned*>(ws + kRedMaxBlocks);
+  double* o = (double*)out;
   if (dtype == kF64) {
-    if (op == kRedSum) rand_reduce_f64<kRedSum><<<g, kRedBlock, 0, stream>>>(n, k0, k1, offset, lo, hi - lo, ws);
-    else rand_reduce_f64<kRedSquareSum><<<g, kRedBlock, 0, stream>>>(n, k0, k1, offset, lo, hi - lo, ws);
+    if (op == kRedSum) rand_reduce_f64<kRedSum><<<g, kRedBlock, 0, stream>>>(n, k0, k1, offset, lo, hi - lo, ws, t, o);
+    else rand_reduce_f64<kRedSquareSum><<<g, kRedBlock, 0, stream>>>(n, k0, k1, offset, lo, hi - lo, ws, t, o);
   } else {
     if (op == kRedSum)
-      rand_reduce_f32<kRedSum><<<g, kRedBlock, 0, stream>>>(n, k0, k1, offset, (float)lo, (float)(hi - lo), ws);
+      rand_reduce_f32<kRedSum><<<g, kRedBlock, 0, stream>>>(n, k0, k1, offset, (float)lo, (float)(hi - lo), ws, t, o);
     else
-      rand_reduce_f32<kRedSquareSum><<<g, kRedBlock, 0, stream>>>(n, k0, k1, offset, (float)lo, (float)(hi - lo), ws);
+      rand_reduce_f32<kRedSquareSum><<<g, kRedBlock, 0, stream>>>(n, k0, k1, offset, (float)lo, (float)(hi - lo), ws, t,
+                                                                  o);
   }
-  if (op == kRedSum) reduce_stage2<kRedSum><<<1, kRedBlock, 0, stream>>>(ws, (int)g, (double*)out);
-  else reduce_stage2<kRedSquareSum><<<1, kRedBlock, 0, stream>>>(ws, (int)g, (double*)out);
   return launch_status();
 }
 
-BK_API int bk_reduce_workspace_bytes() { return kRedMaxBlocks * (int)sizeof(double); }
+// partials, then the completion ticket (its own 256 B)
+BK_API int bk_reduce_workspace_bytes() { return kRedMaxBlocks * (int)sizeof(double) + 256; }
+
+// A fresh workspace's tickets must read zero (each launch re-arms its own).
+BK_API int bk_reduce_workspace_init(void* workspace, hipStream_t stream) {
+  if (!workspace) return kBadArgument;
+  if (hipMemsetAsync((char*)workspace + kRedMaxBlocks * sizeof(double), 0, 256, stream) != hipSuccess)
+    return kLaunchFailed;
+  return kOk;
+}
 
 // out: ONE double on the device.  workspace: bk_reduce_workspace_bytes() bytes.
-// b is only read for kRedDot (same length and dtype as a).
+// b is only read for kRedDot and kRedMaxAbsDiff (same length and dtype as a).
 BK_API int bk_reduce(int op, int dtype, const void* a, const void* b, int64_t n, void* workspace, void* out,
                      hipStream_t stream) {
-  if (!a || !out || !workspace || n < 0 || op < 0 || op >= kRedCount || (op == kRedDot && !b)) return kBadArgument;
+  if (!a || !out || !workspace || n < 0 || op < 0 || op >= kRedCount || ((op == kRedDot || op == kRedMaxAbsDiff) && !b)) return kBadArgument;
   using Ops = std::make_integer_sequence<int, kRedCount>;
   switch (dtype) {
     case kF64: return dispatch_reduce<double>(op, a, b, n, (double*)workspace, (double*)out, stream, Ops{});
@@ -374,7 +467,17 @@ BK_API int bk_reduce(int op, int dtype, const void* a, const void* b, int64_t n,
   return kBadArgument;
 }
 
-BK_API int64_t bk_reduce_axis_workspace_bytes() { return kAxisWsDoubles * (int64_t)sizeof(double); }
+BK_API int64_t bk_reduce_axis_workspace_bytes() {
+  return kAxisWsDoubles * (int64_t)sizeof(double) + kAxisTickets * (int64_t)sizeof(unsigned);
+}
+
+BK_API int bk_reduce_axis_workspace_init(void* ws, hipStream_t stream) {
+  if (!ws) return kBadArgument;
+  if (hipMemsetAsync((char*)ws + kAxisWsDoubles * sizeof(double), 0, kAxisTickets * sizeof(unsigned), stream) !=
+      hipSuccess)
+    return kLaunchFailed;
+  return kOk;
+}
 
 // out[cols] (axis 0) or out[rows] (axis 1) = sum (op 0) or mean (op 1) of
 // x[rows x cols] (row stride ld).  out dtype: f64 for f64 input, f32 for f32

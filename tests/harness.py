@@ -24,13 +24,23 @@ def ensure_native_executor() -> str:
     return os.path.join(ROOT, "bee_code_interpreter_fs_amd", "bin", "bee-executor")
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 class ServiceHarness:
     def __init__(self, tmpdir: str, **overrides) -> None:
+        # ports picked up front, as a deployment configures them: the
+        # executors deny the service's listeners to every sandbox
         base = dict(
             file_storage_path=os.path.join(tmpdir, "files"),
             sandbox_root=os.path.join(tmpdir, "sandboxes"),
-            grpc_listen_addr="127.0.0.1:0",
-            http_listen_addr="127.0.0.1:0",
+            grpc_listen_addr=f"127.0.0.1:{free_port()}",
+            http_listen_addr=f"127.0.0.1:{free_port()}",
             gpu_ids=[],
             workers_per_gpu_target=2,
             executor_backend="local",
@@ -63,7 +73,8 @@ class ServiceHarness:
         self.grpc_port = self.ctx.grpc_server.bind(self.config.grpc_listen_addr)
         await self.ctx.grpc_server.start()
         self.http = uvicorn.Server(
-            uvicorn.Config(self.ctx.http_server, host="127.0.0.1", port=0, loop="asyncio", log_level="warning")
+            uvicorn.Config(self.ctx.http_server, host="127.0.0.1", port=int(self.config.http_listen_addr.rpartition(":")[2]),
+                           loop="asyncio", log_level="warning")
         )
         self.http.install_signal_handlers = lambda: None
         self.http_task = asyncio.ensure_future(self.http.serve())

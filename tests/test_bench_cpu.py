@@ -28,3 +28,45 @@ def test_single_process_multi_gpu_run_scales_offered_load():
     assert out["per_gpu_rps"] == round(out["value"] / 2, 3)
     assert out["cpu_cores_busy"]["value"] > 0
     assert {"metric", "value", "unit", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling"} <= set(out)
+
+
+def _bf16(x):
+    """Round float32 to bfloat16 (nearest even), back as float32."""
+    import numpy as np
+
+    b = np.asarray(x, dtype=np.float32).view(np.uint32)
+    b = (b + 0x7FFF + ((b >> 16) & 1)) & 0xFFFF0000
+    return b.astype(np.uint32).view(np.float32)
+
+
+def test_headline_checks_bite():
+    """the payload's checks, emulated on the host.
+
+    * Result (sum of 1e8 U^2) is accepted within 6 sigma (sigma = sqrt(n *
+      4/45) ~ 2981), not the old +-5e4 (~17 sigma);
+    * the GEMM check compares every row sum of C = bf16(A @ B.T) with
+      A @ bf16(colsum(B)): a correct 4096^3 bf16 GEMM passes with a wide
+      margin, one zeroed 256x256 tile fails."""
+    import numpy as np
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert 2900 < bench.RESULT_SIGMA < 3050
+    assert bench.result_ok(bench.EXPECTED + 5.9 * bench.RESULT_SIGMA)
+    assert not bench.result_ok(bench.EXPECTED + 6.1 * bench.RESULT_SIGMA)
+    assert not bench.result_ok(bench.EXPECTED - 2e4) and not bench.result_ok(0.0)
+
+    rng = np.random.default_rng(7)
+    n = 4096
+    a = _bf16(rng.uniform(-1, 1, (n, n)).astype(np.float32))
+    b = _bf16(rng.uniform(-1, 1, (n, n)).astype(np.float32))
+    c = _bf16(a @ b.T)                                   # f32 accumulate, bf16 out
+    s = _bf16(b.sum(axis=0, dtype=np.float64).astype(np.float32))  # colsum(B), f64-accumulated, bf16 row
+    ref = a.astype(np.float64) @ s.astype(np.float64)
+    err = np.abs(c.sum(axis=1, dtype=np.float64) - ref).max()
+    assert bench.gemm_row_ok(err) and err < bench.GEMM_ROW_TOL / 4, err
+    bad = c.copy()
+    bad[256:512, 1024:1280] = 0.0                        # one corrupt tile
+    err_bad = np.abs(bad.sum(axis=1, dtype=np.float64) - ref).max()
+    assert not bench.gemm_row_ok(err_bad), err_bad

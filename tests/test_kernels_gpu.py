@@ -4,8 +4,12 @@ Run on an MI355X: ``python -m pytest tests -m gpu``.  Each kernel is checked
 against numpy / torch computed in fp32 (bf16 inputs) or fp64.
 """
 
+import os
+
 import numpy as np
 import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -345,8 +349,9 @@ def test_gemm_edge_kernel_unaligned_shapes(gpu, shape, out):
     c0 = torch.empty(M, ldc, device="cuda", dtype=dt).uniform_(-1, 1, generator=g)
     c = c0.clone()
     lib = _native.lib()
-    # K % 64 == 0 and enough 256^2 tiles: the 4-wave kernel's edge mode (7); else the 128^2 edge kernel (6)
-    want = 7 if ((M + 255) // 256) * ((N + 255) // 256) >= 128 else 6
+    # N <= 16: the skinny GEMV kernel (8); K % 64 == 0 and enough 256^2 tiles: the 4-wave kernel's edge
+    # mode (7); else the 128^2 edge kernel (6)
+    want = 8 if N <= 16 else 7 if ((M + 255) // 256) * ((N + 255) // 256) >= 128 else 6
     assert lib.bk_gemm_bf16_pick(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, ldc,
                                  0 if out == "float32" else 2) == want
     rc = lib.bk_gemm_bf16_tn_variant(a.data_ptr(), bt.data_ptr(), c.data_ptr(), M, N, K, K, K, ldc, 0.75, 0.5,
@@ -604,3 +609,103 @@ def test_matmul_row_major_b(gpu, nn, monkeypatch):
         bb = b.astype("float32").numpy().astype(np.float64)
         ref = ab @ bb
         assert np.abs(c - ref).max() < 1e-3 * max(1.0, np.abs(ref).max()), (M, N, K)
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 8, 16])
+@pytest.mark.parametrize("out", ["float32", "bfloat16"])
+def test_gemv_shapes_take_the_skinny_kernel(gpu, n, out):
+    """N <= 16 (matrix-vector products, the payload's row check): variant 8,
+    A read once, against fp64 numpy."""
+    from bee_code_interpreter_fs_amd.ops import _native
+
+    m, k = 4096, 4096
+    rng = np.random.default_rng(n)
+    a_h = _bf16_round(rng.uniform(-1, 1, (m, k)).astype(np.float32))
+    bt_h = _bf16_round(rng.uniform(-1, 1, (n, k)).astype(np.float32))
+    a, bt = gpu.asarray(a_h, "bfloat16"), gpu.asarray(bt_h, "bfloat16")
+    lib = _native.lib()
+    assert lib.bk_gemm_bf16_pick(a.ptr, bt.ptr, a.ptr, m, n, k, k, k, n, 0 if out == "float32" else 2) == 8
+    c = gpu.gemm_bf16_tn(a, bt, out_dtype=out).numpy().astype(np.float64)
+    ref = a_h.astype(np.float64) @ bt_h.astype(np.float64).T
+    atol = 2e-3 * np.sqrt(k) if out == "float32" else 1e-2 * np.abs(ref).max()
+    np.testing.assert_allclose(c, ref, rtol=1e-2, atol=atol)
+
+
+def test_headline_gemm_check_catches_one_corrupt_tile(gpu):
+    """The benchmark payload's row check (examples/benchmark_numpy_gpu.py,
+    bench.gemm_row_ok) on the real kernels: a correct 4096^3 GEMM passes,
+    the same C with one 256x256 tile zeroed fails."""
+    import bench
+
+    ns = {"__bk__": gpu, "__name__": "payload"}
+    src = open(os.path.join(ROOT, "examples", "benchmark_numpy_gpu.py")).read()
+    exec(compile(src.split("start_time = time.time()")[0].replace("import beekern as bk", "bk = __bk__"),
+                 "payload", "exec"), ns)
+    result, checksum, a, b, rows = ns["gpu_intensive_computation"]()
+    assert bench.result_ok(float(result))
+    err = float(ns["gemm_row_error"](a, b, rows))
+    assert bench.gemm_row_ok(err), err
+    host = gpu.matmul(a, b.T).numpy()
+    assert abs(float(checksum) - float(host.astype(np.float64).sum())) < 1.0
+    host[1024:1280, 2048:2304] = 0.0
+    bad_rows = gpu.sum(gpu.asarray(host, "bfloat16"), axis=1)
+    err_bad = float(ns["gemm_row_error"](a, b, bad_rows))
+    assert not bench.gemm_row_ok(err_bad), err_bad
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32", "bfloat16"])
+@pytest.mark.parametrize("n", [1, 63, 4096, 1_000_003])
+def test_max_abs_diff(gpu, dtype, n):
+    rng = np.random.default_rng(n)
+    a_h = rng.standard_normal(n)
+    b_h = a_h + rng.standard_normal(n) * 1e-3
+    b_h[n // 2] += 5.0  # the one outlier
+    a, b = gpu.asarray(a_h, dtype), gpu.asarray(b_h, dtype)
+    want = np.abs(a.numpy().astype(np.float64) - b.numpy().astype(np.float64)).max()
+    assert float(gpu.max_abs_diff(a, b)) == pytest.approx(want, rel=1e-6)
+
+
+SEGMENT_PROBE = r"""
+import ctypes, random
+import numpy as np
+from bee_code_interpreter_fs_amd import ops
+from bee_code_interpreter_fs_amd.ops import _native
+ops.init(0)
+lib = _native.lib()
+lib.bk_reserve.argtypes = [ctypes.c_int64]
+assert lib.bk_reserve(1 << 30) == 0
+rng = random.Random(5)
+live = {}
+for step in range(400):
+    if live and (rng.random() < 0.45 or len(live) > 40):
+        k = rng.choice(list(live))
+        arr, val = live.pop(k)
+        assert float(ops.amax(arr)) == val and float(ops.amin(arr)) == val, (step, k)  # nobody wrote over it
+        del arr
+    else:
+        n = rng.choice([1 << 18, 3 << 19, 1 << 20, 5 << 20, 1 << 23, 3 << 24]) // 8  # bytes -> f64 elements
+        val = float(step)
+        live[step] = (ops.full((n,), val, "float64"), val)
+for k, (arr, val) in live.items():
+    assert float(ops.amax(arr)) == val and float(ops.amin(arr)) == val
+live.clear()
+ops.synchronize()
+st = (ctypes.c_int64 * 4)()
+lib.bk_memory_stats(st)
+# everything back and coalesced: one 1 GiB block fits again without a new segment
+big = ops.empty(((1 << 30) - (2 << 20)) // 8, "float64")
+lib.bk_memory_stats(st)
+print("ok", st[0], st[1])
+"""
+
+
+def test_broker_segment_allocator_reuses_and_coalesces(gpu):
+    """bk_reserve switches large blocks to best-fit segments (what the kernel
+    broker runs on): random alloc / free churn over 256 KiB..48 MiB blocks
+    never hands out overlapping memory, and once everything is freed the
+    segment coalesces back into one extent (a ~1 GiB block fits in it)."""
+    import subprocess
+    import sys
+
+    p = subprocess.run([sys.executable, "-c", SEGMENT_PROBE], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0 and p.stdout.startswith("ok"), p.stdout + p.stderr[-3000:]

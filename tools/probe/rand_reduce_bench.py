@@ -15,7 +15,7 @@ s = torch.cuda.current_stream().cuda_stream
 rr = lib.bk_rand_reduce
 rr.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
                ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-ws = torch.empty(lib.bk_reduce_workspace_bytes() // 8 + 1, dtype=torch.float64, device="cuda")
+ws = torch.zeros(lib.bk_reduce_workspace_bytes() // 8 + 1, dtype=torch.float64, device="cuda")  # tickets start at 0
 out = torch.empty(1, dtype=torch.float64, device="cuda")
 
 
