@@ -105,6 +105,10 @@ async def main() -> None:
     ctx = ApplicationContext(config)
     stop = _install_stop(asyncio.get_running_loop())
     await ctx.start()
+    backend = ctx.code_executor
+    if (config.startup_warm_timeout_s > 0 and hasattr(backend, "wait_warm")
+            and not os.environ.get("BEE_FRONTEND_ATTACH")):
+        await backend.wait_warm(config.startup_warm_timeout_s)
     try:
         await _serve(ctx, stop)
     finally:
@@ -144,6 +148,8 @@ async def supervise(config: Config, n_frontends: int) -> None:
     if hasattr(backend, "deny_ports"):
         backend.deny_ports = sorted(set(backend.deny_ports) | {gport, hport, *replica_ports})
     await backend.start()
+    if config.startup_warm_timeout_s > 0 and hasattr(backend, "wait_warm"):
+        await backend.wait_warm(config.startup_warm_timeout_s)
     env = dict(os.environ)
     env.update(
         {

@@ -551,7 +551,7 @@ def power(a, b): return _binary("power", a, b)
 # 7-10% faster than the [K][N] one.  The pass costs ~600/M of the GEMM, so
 # reading in place wins below M ~ 6k.  Measured on MI355X, TFLOP/s, [K][N]
 # kernel vs transpose + TN (hipBLASLt's NN in brackets,
-# profiles/r2_s3_gemm_nn_sweep.log):
+# profiles/archive/r2_s3_gemm_nn_sweep.log):
 #   M=N=4096,  K=512..4096: 715/949/1132/1229/1298 vs 574/771/1029/1154/1218
 #                           (659/935/1140/1256/1302)
 #   2048x8192x2048: 1211 vs 1014 (1195)

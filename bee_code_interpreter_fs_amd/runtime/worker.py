@@ -596,7 +596,7 @@ def _serve(cwd: str, chan: _Chan) -> None:
         # BEE_PREFAULT=1: exercise the request path's Python machinery while
         # pooled.  Off by default since the request-independent setup moved
         # into the pooled phase: on MI355X it then cost 0.3-0.7 ms of CPU per
-        # Execute and bought no latency (profiles/r2_prefault_thp_ab.log)
+        # Execute and bought no latency (profiles/archive/r2_prefault_thp_ab.log)
         if os.environ.get("BEE_PREFAULT", "0") == "1":
             _prefault()
         _prefault_scientific()

@@ -143,7 +143,7 @@ class ExecutorProcess:
             # on MI355X 2 queues cut the in-sandbox GPU time of 8 concurrent
             # headline Executes from 1.04-1.12 to 0.93-0.96 ms, but moved
             # neither RPS nor p50 beyond box noise (2503 vs 2580, 2437 vs 2329
-            # RPS means in two interleaved series; profiles/r2_s3_hw_queues_ab.log)
+            # RPS means in two interleaved series; profiles/archive/r2_s3_hw_queues_ab.log)
             if os.environ.get("BEE_EXECUTOR_HW_QUEUES"):
                 env["GPU_MAX_HW_QUEUES"] = os.environ["BEE_EXECUTOR_HW_QUEUES"]
         self.log_path = os.path.join(run_dir, "executor.log")

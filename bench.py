@@ -103,7 +103,7 @@ def parse_args():
     p.add_argument("--steps", type=int, default=600)  # per client: 4800 Executes on 1 GPU, ~2 s
     # untimed: 400 Executes on 1 GPU bring the allocator caches, sandbox
     # pools and zygote page state to steady state (30 timed steps after 10
-    # warm-up steps ran at 1836 RPS vs ~2700 sustained, profiles/r2_s3_bench_suite.jsonl)
+    # warm-up steps ran at 1836 RPS vs ~2700 sustained, profiles/archive/r2_s3_bench_suite.jsonl)
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--concurrency", type=int, default=8, help="closed-loop clients per GPU")
     p.add_argument("--pool-target", type=int, default=16, help="warm minimal sandboxes per GPU")
@@ -234,9 +234,9 @@ def start_service(tmp: str, n_gpus: int, args):
     gport, hport = free_port(), free_port()
     # three front-end replicas per GPU (at most 16): one Python gRPC process
     # saturates a core at ~2.2k Execute/s (2235 -> 2378 RPS with a second
-    # replica on one GPU, profiles/r2_bench_frontends_ab.log); a third took
+    # replica on one GPU, profiles/archive/r2_bench_frontends_ab.log); a third took
     # p50 down in 3 of 3 interleaved pairs, 2794 vs 2734 RPS mean
-    # (profiles/r2_s3_frontends3_ab.log)
+    # (profiles/archive/r2_s3_frontends3_ab.log)
     frontends = args.frontends or min(16, 3 * max(1, n_gpus))
     env = dict(os.environ)
     env.update(

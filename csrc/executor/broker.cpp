@@ -233,6 +233,11 @@ class HipDevice final : public broker::Device {
     bk.malloc_(&c->scalar, 256);
     void* page = nullptr;
     if (hipHostMalloc(&page, 64, hipHostMallocCoherent) == hipSuccess) c->slot = (double*)page;
+    hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming);
+    for (int i = 0; i < 4; ++i) {  // the deferred-free events a session typically has in flight
+      hipEvent_t ev = nullptr;
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) c->spare_events.push_back(ev);
+    }
     return c;
   }
   void give_stream(void* p) override {
@@ -355,7 +360,7 @@ class HipDevice final : public broker::Device {
   // default: relative backoff (2 us, then 1/8 of the wait so far, <= 50 us):
   // A/B on MI355X, 4 interleaved runs each, broker CPU 0.30-0.33 vs
   // 0.34-0.35 ms per Execute, RPS 2500-2665 vs 2466-2550
-  // (profiles/r2_s3_broker_poll_ab.log)
+  // (profiles/archive/r2_s3_broker_poll_ab.log)
   long poll_min_ns_ = 2000, poll_max_ns_ = 50000;
   int poll_div_ = 8;
   bool poll_set_ = (poll_schedule(&poll_min_ns_, &poll_max_ns_, &poll_div_), true);
@@ -381,6 +386,22 @@ bool KernelBroker::start(std::string* err) {
   const double t0 = mono_ms();
   if (!dev_->init(err)) return false;
   BEE_INFO("kernel broker: HIP context on %s ready in %.0f ms", dev_->arch().c_str(), mono_ms() - t0);
+  {
+    // the per-session GPU resources (stream, reduction workspace, pinned
+    // result slot, wait event) for as many concurrent sessions as the GPU
+    // admits, created now: a fresh broker used to create them on its first
+    // requests, ms each (BEE_BROKER_PREWARM_SESSIONS, default 16)
+    const char* pw = getenv("BEE_BROKER_PREWARM_SESSIONS");
+    const int n = pw && *pw ? atoi(pw) : 16;
+    const double tp = mono_ms();
+    std::vector<void*> ctxs;
+    for (int i = 0; i < n; ++i) ctxs.push_back(dev_->take_stream());
+    for (void* c : ctxs) {
+      dev_->sync(c);
+      dev_->give_stream(c);
+    }
+    BEE_INFO("kernel broker: %d session contexts ready in %.0f ms", n, mono_ms() - tp);
+  }
   listen_fd_ = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
   sockaddr_un addr{};
   addr.sun_family = AF_UNIX;

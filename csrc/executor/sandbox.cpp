@@ -1709,6 +1709,7 @@ Json SandboxPool::status() {
   j.set("target", cfg_.target);
   j.set("light_target", target_of(kLight));
   j.set("min_target", target_of(kMin));
+  j.set("min_cpu_target", target_of(kMinCpu));
   Json cpu = Json::object();
   for (int i = 0; i < kCpuParts; ++i) cpu.set(kCpuPartNames[i], g_cpu_ns[i].load() / 1e6);
   j.set("cpu_ms", cpu);

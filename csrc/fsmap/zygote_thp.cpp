@@ -6,7 +6,7 @@
 // It can only do that once Python runs the zygote module: by then interpreter
 // start-up has filled ~3 arenas on 4 KB pages -- the builtins, sys, site and
 // encodings objects that every sandbox touches (BEE_DEBUG_ZYGOTE_MEM,
-// profiles/r2_s3_zygote_mem_small_pages.log).  Loaded with LD_PRELOAD, this
+// profiles/archive/r2_s3_zygote_mem_small_pages.log).  Loaded with LD_PRELOAD, this
 // constructor runs before the interpreter initialises and installs the same
 // arena allocator then, when the executor asks for it in the zygote's
 // environment (BEE_ZYGOTE_THP_EARLY=1; the zygote drops the variable at once,

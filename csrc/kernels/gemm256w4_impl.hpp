@@ -1,6 +1,6 @@
 // bf16 GEMM, 256x256 block tile, FOUR waves of 128x128: C = alpha * A . Bt^T (+ beta C)
 //
-// Why four waves (measured, profiles/r1_gemm_lab.log + PMC): the 8-wave
+// Why four waves (measured, profiles/archive/r1_gemm_lab.log + PMC): the 8-wave
 // 128x64-per-wave kernel (gemm256_impl.hpp) issues 238 ds_read_b128 per CU
 // per K-tile and runs 8 barriers per K-tile; its MFMA pipes were busy 58% of
 // the cycles, and moving its operands into L2 (diagnostic variant) bought only
@@ -137,7 +137,7 @@ __device__ __forceinline__ srd4 srd_words(const void* base, uint32_t bytes) {
 // its direct-to-LDS loads this way because the compiler, seeing an LDS DMA in
 // flight, puts an s_waitcnt vmcnt(0) before every ds_read_b64_tr_b16 (whose
 // memory operand it cannot disambiguate) -- 14x the wait cycles
-// (profiles/r2_gemm_pmc_4096.jsonl).  Hidden from the compiler, the loads are
+// (profiles/archive/r2_gemm_pmc_4096.jsonl).  Hidden from the compiler, the loads are
 // ordered by the schedule's own s_waitcnt vmcnt + s_barrier, as before.
 __device__ __forceinline__ void glds_raw(const srd4& w, const uint16_t* lds, int voff, int soff) {
   const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(lds_void_ptr)(lds));

@@ -3,7 +3,7 @@
 //   * the 4-wave kernel (gemm256w4_impl.hpp, 128x128 per wave) with inline-asm
 //     MFMAs on AGPR accumulators and a hand-interleaved load/MFMA schedule
 // Both schedules are winners of tools/gemm_lab.py on MI355X
-// (profiles/r1_gemm_lab.log): the 4-wave kernel issues half the LDS reads per
+// (profiles/archive/r1_gemm_lab.log): the 4-wave kernel issues half the LDS reads per
 // MFMA and wins from K >= 256 on (4096^3: 1401 vs 1259 TFLOP/s); the 8-wave
 // kernel wins short-K shapes, where the 4-wave prologue/epilogue dominate.
 #include "gemm256_impl.hpp"

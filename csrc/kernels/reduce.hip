@@ -11,7 +11,7 @@
 // so results are bitwise reproducible run to run.  (A second single-block
 // launch used to do the fold: under concurrent sandboxes it queued behind
 // other tenants' GEMMs holding every CU -- 25 us mean for a 1.8 us kernel,
-// profiles/r2_s3_final_served_path_kernels.csv.)
+// profiles/archive/r2_s3_final_served_path_kernels.csv.)
 #include "bk_common.hpp"
 #include "bk_philox.hpp"
 

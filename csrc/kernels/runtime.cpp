@@ -15,7 +15,7 @@
 //    hipMallocs) and given back with coalescing, so ANY large size is served
 //    without a driver call once a segment exists.  A hipMalloc of a large
 //    buffer takes milliseconds (2.5-18 ms on a cold cache in the kernel
-//    broker, profiles/r2_s3_served_path_ranges.csv) and an exact-size cache
+//    broker, profiles/archive/r2_s3_served_path_ranges.csv) and an exact-size cache
 //    only warms up per size and per concurrency level: a freshly started
 //    broker served its first hundreds of requests 20-35% slower.  The broker
 //    reserves its first segment at start-up (bk_reserve).
@@ -388,7 +388,7 @@ BK_API int bk_transpose_bf16(const void*, void*, int, int, int, int, hipStream_t
 // Run one tiny launch from every kernel module so HIP loads the code objects
 // now: with deferred loading the first launch from each module costs tens of
 // ms (measured in the served path: the first bk.rand 128 ms, the first
-// rand_reduce 34 ms; profiles/r1_served_path_final_ranges.csv), which a
+// rand_reduce 34 ms; profiles/archive/r1_served_path_final_ranges.csv), which a
 // long-lived process (the kernel broker) should pay at startup, not on a
 // request.  Returns the first failure.
 BK_API int bk_preload(hipStream_t stream) {
