@@ -23,8 +23,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NAMES = {0: "round1", 1: "keep_b0", 2: "round1_nostagger", 3: "keep_b0_nostagger", 4: "diag_round1_l2", 5: "diag_keep_b0_l2",
          6: "w4", 7: "w4_pinned", 8: "w4_interleaved", 9: "w4_nocarry", 10: "w4_directstore",
          11: "w4_asm_interleaved", 12: "w4_asm_nocarry", 13: "w4_asm_early", 14: "w4_asm_reads_early",
-         15: "w4_asm_reads_early_glds_early", 16: "w4_asm_group2", 17: "w4_asm_group8", 18: "w4_asm_group16"}
-DIAG = {4, 5}
+         15: "w4_asm_reads_early_glds_early", 16: "w4_asm_group2", 17: "w4_asm_group8", 18: "w4_asm_group16",
+         19: "w4_asm_3bar", 20: "w4_asm_3bar_group8", 21: "w4_asm_3bar_edge",
+         22: "w4_asm_3bar_spread", 23: "w4_asm_3bar_spread_edge",
+         24: "w4_asm_directstore", 25: "diag_w4_asm_no_epilogue",
+         26: "w4_asm_swapab", 27: "w4_asm_swapab_edge", 28: "diag_w4_asm_swapab_no_epilogue"}
+DIAG = {4, 5, 25, 28}
 PROD = None
 
 

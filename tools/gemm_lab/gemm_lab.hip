@@ -30,7 +30,17 @@ constexpr int kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave, g4::kNoCarry, g4::
                            g4::kAsmMfma | g4::kInterleave | g4::kReadsEarly | g4::kEarlyGlds,
                            g4::kAsmMfma | g4::kInterleave | g4::kGroup2,
                            g4::kAsmMfma | g4::kInterleave | g4::kGroup8,
-                           g4::kAsmMfma | g4::kInterleave | g4::kGroup16};
+                           g4::kAsmMfma | g4::kInterleave | g4::kGroup16,
+                           g4::kAsmMfma | g4::kInterleave | g4::kThreeBar,
+                           g4::kAsmMfma | g4::kInterleave | g4::kThreeBar | g4::kGroup8,
+                           g4::kAsmMfma | g4::kInterleave | g4::kThreeBar | g4::kEdge,
+                           g4::kAsmMfma | g4::kInterleave | g4::kThreeBar | g4::kSpread,
+                           g4::kAsmMfma | g4::kInterleave | g4::kThreeBar | g4::kSpread | g4::kEdge,
+                           g4::kAsmMfma | g4::kInterleave | g4::kDirectStore,
+                           g4::kAsmMfma | g4::kInterleave | g4::kDiagNoEpilogue,
+                           g4::kAsmMfma | g4::kInterleave | g4::kSwapAB,
+                           g4::kAsmMfma | g4::kInterleave | g4::kSwapAB | g4::kEdge,
+                           g4::kAsmMfma | g4::kInterleave | g4::kSwapAB | g4::kDiagNoEpilogue};
 template <int I>
 void run_w4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool bf,
             hipStream_t s) {
@@ -63,6 +73,16 @@ BK_API int gemmlab_run(int variant, const void* A, const void* Bt, void* C, int 
     case 16: run_w4<10>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 17: run_w4<11>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 18: run_w4<12>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 19: run_w4<13>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 20: run_w4<14>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 21: run_w4<15>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 22: run_w4<16>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 23: run_w4<17>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 24: run_w4<18>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 25: run_w4<19>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 26: run_w4<20>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 27: run_w4<21>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 28: run_w4<22>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     default: return kBadArgument;
   }
   return launch_status();
