@@ -2,8 +2,8 @@
 
 Lifecycle (driven by the native executor, csrc/executor/sandbox.cpp):
 
-1. ``setsid`` — the worker leads its own process group, so the executor can
-   kill everything the user code started with one ``killpg``;
+1. ``setsid`` — the worker leads its own session and process group, so the
+   executor can kill everything the user code started with one ``killpg``;
 2. apply the sandbox environment (GPU pin via ``HIP_VISIBLE_DEVICES``, dirs,
    HBM quota) — HIP is still uninitialised in the zygote, so this is legal;
 3. connect to the executor, say ``hello``;
@@ -535,7 +535,10 @@ def worker_main(spawn: dict) -> None:
     try:
         _DEBUG = os.environ.get("BEE_DEBUG_NEW_MODULES") == "1"
         _cpu_stamp("forked")
-        os.setsid()
+        if os.environ.get("BEE_SANDBOX_SETSID") == "0":
+            os.setpgid(0, 0)  # a group of its own in the zygote's session (boot_child)
+        else:
+            os.setsid()
         # this sandbox's tree keeps its orphans (a double fork re-parents to
         # us, not to the zygote): the executor accounts and kills them with it
         import ctypes

@@ -58,7 +58,8 @@ void usage() {
           "                    [--mem-limit BYTES] [--cpus LIST] [--gang-grace S]\n"
           "                    [--hbm-watchdog-ms MS] [--hbm-slack BYTES] [--max-inflight N] [--hbm-capacity BYTES]\n"
           "                    [--admit-timeout S] [--sandbox-memory BYTES] [--sandbox-tasks N] [--sandbox-cpus C]\n"
-          "                    [--monitor-ms MS] [--deny-ports P1,P2,...]\n");
+          "                    [--monitor-ms MS] [--deny-ports P1,P2,...]\n"
+          "                    [--cgroup auto|require|off|fake] [--cgroup-root DIR]\n");
 }
 
 bool resolve_pod_path(const PoolConfig& cfg, const std::string& url_path, std::string* real, std::string* err) {
@@ -152,6 +153,8 @@ int main(int argc, char** argv) {
     else if (a == "--sandbox-cpus") cfg.sandbox_cpus = atof(val().c_str());
     else if (a == "--monitor-ms") cfg.monitor_ms = atoi(val().c_str());
     else if (a == "--deny-ports") cfg.deny_ports = val();
+    else if (a == "--cgroup") cfg.cgroup_mode = val();
+    else if (a == "--cgroup-root") cfg.cgroup_root = val();
     else if (a == "-h" || a == "--help") {
       usage();
       return 0;
