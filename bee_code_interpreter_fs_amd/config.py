@@ -153,6 +153,13 @@ class Config:
     # replica to the CPUs of its GPU's NUMA node: "auto" (when the GPUs span
     # several NUMA nodes) or "off"
     numa_affinity: str = "auto"
+    # with a CPU quota far below the CPUs the job may run on (cgroup cpu.max:
+    # 16 CPUs of time on a 256-CPU host), pin the service to this many times
+    # the quota's worth of CPUs, split between the GPU slots (0 = NUMA only).
+    # Off by default: on the MI355X box 2x cut CPU per Execute 15-20% but not
+    # latency -- driver-length runs 1802-2224 vs 2010-2189 RPS, 600-step runs
+    # 1938 / 2443 vs 2343 / 2561 (profiles/r3_cpu_quota_pinning_ab.log)
+    cpu_quota_pin_factor: float = 0.0
     # a gang whose rank failed: seconds the other ranks get to finish before
     # the whole gang is killed (they are usually stuck in a collective)
     gang_failure_grace_s: float = 10.0

@@ -226,7 +226,8 @@ class LocalGpuPoolBackend(CodeExecutor):
             light_target=c.light_workers_per_gpu_target,
             broker=c.broker_enabled,
             light_zygotes=c.light_zygotes_per_gpu,
-            cpus=slot_cpus(gpu) if (c.numa_affinity or "auto").lower() != "off" else None,
+            cpus=slot_cpus(gpu, slots=list(self.gpu_ids), factor=c.cpu_quota_pin_factor)
+            if (c.numa_affinity or "auto").lower() != "off" else None,
             extra_args=["--max-idle", str(c.worker_max_idle_s), "--min-target", str(c.min_workers_per_gpu_target),
                         "--min-zygotes", str(c.min_zygotes_per_gpu),
                         "--min-cpu-target", str(c.min_cpu_workers_per_gpu_target),

@@ -83,21 +83,89 @@ def numa_cpus(node: int, sysfs: str = "/sys") -> List[int]:
     return parse_cpulist(_read(os.path.join(sysfs, "devices", "system", "node", f"node{node}", "cpulist")) or "")
 
 
-def slot_cpus(gpu: Optional[int], sysfs: str = "/sys", allowed: Optional[Set[int]] = None) -> List[int]:
+def cpu_quota(cgroup_fs: str = "/sys/fs/cgroup", proc_cgroup: str = "/proc/self/cgroup") -> float:
+    """CPUs' worth of time per period this process's cgroup may use: the
+    smallest cgroup v2 ``cpu.max`` quota/period on its path (or the v1
+    ``cpu.cfs_quota_us`` / ``cpu.cfs_period_us``); 0 = no quota or unknown."""
+    best = 0.0
+
+    def take(q: float) -> None:
+        nonlocal best
+        if q > 0 and (best == 0 or q < best):
+            best = q
+
+    own = ""
+    for line in (_read(proc_cgroup) or "").splitlines():
+        if line.startswith("0::"):
+            own = line[3:]
+    if own:
+        path = own.strip("/")
+        parts = path.split("/") if path else []
+        for i in range(len(parts), -1, -1):
+            v = _read(os.path.join(cgroup_fs, *parts[:i], "cpu.max"))
+            if v and v.split()[0] != "max":
+                q, per = v.split()[:2]
+                take(int(q) / int(per))
+    for d in ("cpu", "cpu,cpuacct"):
+        q, per = _read(os.path.join(cgroup_fs, d, "cpu.cfs_quota_us")), _read(os.path.join(cgroup_fs, d, "cpu.cfs_period_us"))
+        if q and per and q.lstrip("-").isdigit() and int(q) > 0 and int(per) > 0:
+            take(int(q) / int(per))
+    return best
+
+
+def core_order(cpus: List[int], sysfs: str = "/sys") -> List[int]:
+    """``cpus`` with one logical CPU per physical core first (in CPU order),
+    then the cores' SMT siblings."""
+    first, rest = [], []
+    for c in cpus:
+        sib = parse_cpulist(_read(os.path.join(sysfs, "devices", "system", "cpu", f"cpu{c}", "topology",
+                                               "thread_siblings_list")) or str(c))
+        (first if not sib or c == min(sib) else rest).append(c)
+    return first + rest
+
+
+def slot_cpus(gpu: Optional[int], sysfs: str = "/sys", allowed: Optional[Set[int]] = None,
+              slots: Optional[List[Optional[int]]] = None, quota: Optional[float] = None,
+              factor: float = 2.0) -> List[int]:
     """CPUs for the slot of HIP device ``gpu``: its NUMA node's CPUs that
-    this process may use.  [] = no pinning (unknown topology, one NUMA
-    node, or no overlap with the allowed set)."""
+    this process may use (when the GPUs span several NUMA nodes), and --
+    when the job's CPU quota (``cpu_quota``) is far below the CPUs it may run
+    on -- only ``factor`` x quota of them in all, split between the slots
+    (``slots``: every slot's GPU) and physical cores first.  A 16-CPU quota on
+    a 256-CPU host otherwise spreads the service over 16 L3 slices and lets
+    bursts of runnable threads spend the quota early in a period and stall
+    until its end (cpu.stat nr_throttled).  On MI355X, pinned to 32 CPUs:
+    4.8-5.2 vs 5.8-7.2 ms of CPU per Execute, throughput within the boxes'
+    noise on driver-length runs and lower on 600-step runs
+    (profiles/r3_cpu_quota_pinning_ab.log), so the service's default factor
+    is 0 (config.cpu_quota_pin_factor).  [] = no pinning."""
     if gpu is None:
-        return []
-    numa = gpu_numa_nodes(sysfs)
-    if gpu >= len(numa) or numa[gpu] < 0 or len({n for n in numa if n >= 0}) < 2:
         return []
     if allowed is None:
         try:
             allowed = set(os.sched_getaffinity(0))
         except (AttributeError, OSError):
             allowed = None
-    cpus = numa_cpus(numa[gpu], sysfs)
-    if allowed is not None:
-        cpus = [c for c in cpus if c in allowed]
-    return cpus
+    numa = gpu_numa_nodes(sysfs)
+    by_numa = gpu < len(numa) and numa[gpu] >= 0 and len({n for n in numa if n >= 0}) >= 2
+    cpus: List[int] = []
+    if by_numa:
+        cpus = numa_cpus(numa[gpu], sysfs)
+        if allowed is not None:
+            cpus = [c for c in cpus if c in allowed]
+    q = cpu_quota() if quota is None else quota
+    if q > 0 and factor > 0 and allowed:
+        budget = max(2, int(factor * q + 0.999))
+        if budget < len(allowed):
+            slots = [g for g in (slots or [gpu]) if g is not None] or [gpu]
+            per = max(2, -(-budget // len(slots)))
+            if by_numa:  # the slots of this NUMA node split its CPUs
+                peers = [g for g in slots if g < len(numa) and numa[g] == numa[gpu]]
+                pool = cpus
+            else:
+                peers, pool = slots, sorted(allowed)
+            k = peers.index(gpu) if gpu in peers else 0
+            ordered = core_order(pool, sysfs)
+            chunk = ordered[k * per:(k + 1) * per] or ordered[:per]
+            return sorted(chunk)
+    return cpus if by_numa else []

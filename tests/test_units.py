@@ -461,9 +461,9 @@ def test_numa_topology_and_slot_cpus(tmp_path):
     assert t.format_cpulist([11, 10, 8, 3, 2, 1, 0]) == "0-3,8,10-11"
     _fake_sysfs(str(tmp_path), [0, 0, 0, 0, 1, 1, 1, 1])
     assert t.gpu_numa_nodes(str(tmp_path)) == [0, 0, 0, 0, 1, 1, 1, 1]
-    assert t.slot_cpus(0, str(tmp_path), allowed=set(range(16))) == [0, 1, 2, 3, 8, 9, 10, 11]
-    assert t.slot_cpus(6, str(tmp_path), allowed=set(range(16))) == [4, 5, 6, 7, 12, 13, 14, 15]
-    assert t.slot_cpus(6, str(tmp_path), allowed={0, 1, 5}) == [5]  # only CPUs this process may use
+    assert t.slot_cpus(0, str(tmp_path), allowed=set(range(16)), quota=0) == [0, 1, 2, 3, 8, 9, 10, 11]
+    assert t.slot_cpus(6, str(tmp_path), allowed=set(range(16)), quota=0) == [4, 5, 6, 7, 12, 13, 14, 15]
+    assert t.slot_cpus(6, str(tmp_path), allowed={0, 1, 5}, quota=0) == [5]  # only CPUs this process may use
     assert t.slot_cpus(None, str(tmp_path)) == []
 
 
@@ -471,5 +471,36 @@ def test_numa_single_node_means_no_pinning(tmp_path):
     from bee_code_interpreter_fs_amd.scheduler import topology as t
 
     _fake_sysfs(str(tmp_path), [0, 0])
-    assert t.slot_cpus(1, str(tmp_path), allowed=set(range(16))) == []
+    assert t.slot_cpus(1, str(tmp_path), allowed=set(range(16)), quota=0) == []
+
+
+def test_cpu_quota_and_quota_pinning(tmp_path):
+    """A 16-CPU cgroup quota on a 256-CPU host: the service is pinned to 2x
+    the quota, physical cores first, split between the GPU slots."""
+    from bee_code_interpreter_fs_amd.scheduler import topology as t
+
+    cg = tmp_path / "cg"
+    (cg / "job" / "leaf").mkdir(parents=True)
+    (cg / "cpu.max").write_text("max 100000\n")
+    (cg / "job" / "cpu.max").write_text("1600000 100000\n")
+    (cg / "job" / "leaf" / "cpu.max").write_text("max 100000\n")
+    pc = tmp_path / "proc_cgroup"
+    pc.write_text("0::/job/leaf\n")
+    assert t.cpu_quota(str(cg), str(pc)) == 16.0
+    pc.write_text("12:cpu:/x\n")  # cgroup v1 only, no quota files
+    assert t.cpu_quota(str(cg), str(pc)) == 0.0
+    # a host of 256 logical CPUs, 128 cores: cpu c and c+128 are siblings, one NUMA node
+    sys_ = tmp_path / "sys"
+    for c in range(256):
+        d = sys_ / "devices" / "system" / "cpu" / f"cpu{c}" / "topology"
+        d.mkdir(parents=True)
+        d.joinpath("thread_siblings_list").write_text(f"{c % 128},{c % 128 + 128}\n")
+    allowed = set(range(256))
+    one = t.slot_cpus(0, str(sys_), allowed=allowed, slots=[0], quota=16.0)
+    assert one == list(range(32)), one  # 32 physical cores, no SMT siblings
+    two = [t.slot_cpus(g, str(sys_), allowed=allowed, slots=[0, 1], quota=16.0) for g in (0, 1)]
+    assert two == [list(range(16)), list(range(16, 32))], two
+    assert t.slot_cpus(0, str(sys_), allowed=allowed, slots=[0], quota=16.0, factor=0) == []  # off: NUMA rules only
+    assert t.slot_cpus(0, str(sys_), allowed=set(range(24)), slots=[0], quota=16.0) == []  # quota ~ what may run
+    assert t.core_order([0, 128, 1, 129], str(sys_)) == [0, 1, 128, 129]
     assert t.gpu_numa_nodes(str(tmp_path / "missing")) == []
