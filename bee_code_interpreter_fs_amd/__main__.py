@@ -17,16 +17,21 @@ from __future__ import annotations
 
 import asyncio
 import json
+import logging
 import os
 import signal
 import socket
 import subprocess
 import sys
+import time
+from typing import List
 
 import uvicorn
 
 from .application_context import ApplicationContext
 from .config import Config
+
+logger = logging.getLogger("bee_service")
 
 
 def _split_addr(addr: str):
@@ -115,6 +120,46 @@ async def main() -> None:
         await ctx.close()
 
 
+# what the self-warm runs: the broker path (allocate, draw, reduce, free) on
+# GPU slots, plain Python on CPU-only ones
+_WARM_GPU = "import beekern as bk\nx = bk.random.rand(1 << 16)\nprint(float(bk.sum(bk.square(x))))\n"
+_WARM_CPU = "print(sum(range(1000)))\n"
+
+
+async def _self_warm(targets: List[str], total: int, concurrency: int, gpu: bool) -> int:
+    """``total`` Executes through the replicas' own ports, ``concurrency``
+    at a time (closed loop), before the service says it is ready; returns how
+    many completed.  Failures only end the warm-up early."""
+    import grpc
+
+    from .models import proto as pb
+
+    chans = [grpc.aio.insecure_channel(t) for t in targets]
+    stubs = [pb.CodeInterpreterServiceStub(c) for c in chans]
+    budget, done = [total], [0]
+    src = _WARM_GPU if gpu else _WARM_CPU
+
+    async def client(i: int) -> None:
+        stub = stubs[i % len(stubs)]
+        while budget[0] > 0:
+            budget[0] -= 1
+            try:
+                r = await stub.Execute(pb.ExecuteRequest(source_code=src), timeout=120)
+            except Exception:  # noqa: BLE001
+                budget[0] = 0
+                return
+            if r.exit_code != 0:
+                budget[0] = 0
+                return
+            done[0] += 1
+
+    try:
+        await asyncio.gather(*(client(i) for i in range(concurrency)))
+    finally:
+        await asyncio.gather(*(c.close() for c in chans), return_exceptions=True)
+    return done[0]
+
+
 def _pin_replica(config: Config, backend, index: int, pid: int) -> None:
     """Replica i runs next to GPU slot i (mod the slot count): its CPU work
     is mostly that slot's sandboxes' RPCs."""
@@ -173,6 +218,12 @@ async def supervise(config: Config, n_frontends: int) -> None:
         for part in line.decode().split():
             if part.startswith("replica_grpc="):
                 replicas.append(part.split("=", 1)[1])
+    if config.startup_self_warm_executions > 0 and replicas:
+        t = time.perf_counter()
+        n_slots = max(1, len(getattr(backend, "slots", None) or [None]))
+        done = await _self_warm(replicas, config.startup_self_warm_executions * n_slots, 8 * n_slots,
+                                gpu=bool(getattr(backend, "gpu_ids", None)))
+        logger.info("self-warm: %d Executes through %d replicas in %.2f s", done, len(replicas), time.perf_counter() - t)
     print(
         f"BEE_SERVICE_READY grpc={ghost}:{gport} http={hhost}:{hport} frontends={n_frontends} "
         f"replicas={','.join(replicas)} slots={json.dumps(json.loads(backend.attach_spec()), separators=(',', ':'))}",

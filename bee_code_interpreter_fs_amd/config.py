@@ -118,6 +118,12 @@ class Config:
     # seconds the service waits for every GPU's sandbox pools to reach target
     # before it reports ready (0 = do not wait)
     startup_warm_timeout_s: float = 300.0
+    # Executes the supervisor drives through its own front-end replicas (per
+    # GPU slot, 8 at a time per slot) before it reports ready: a freshly
+    # started service is 15-25% slower per request for its first ~1-2k
+    # Executes (the replicas' Python, the daemon's and broker's heaps, the
+    # kernel's caches for the fork/exit path grow on first use); 0 = off
+    startup_self_warm_executions: int = 1024
     # default execution timeout in seconds (reference: 60 s, `server.rs:201`)
     default_timeout: float = 60.0
     # where sandboxes (workspace + runtime-packages + logs) are created
