@@ -123,7 +123,7 @@ class Config:
     # started service is 15-25% slower per request for its first ~1-2k
     # Executes (the replicas' Python, the daemon's and broker's heaps, the
     # kernel's caches for the fork/exit path grow on first use); 0 = off
-    startup_self_warm_executions: int = 1024
+    startup_self_warm_executions: int = 3072
     # default execution timeout in seconds (reference: 60 s, `server.rs:201`)
     default_timeout: float = 60.0
     # where sandboxes (workspace + runtime-packages + logs) are created
