@@ -126,10 +126,11 @@ _WARM_GPU = "import beekern as bk\nx = bk.random.rand(1 << 16)\nprint(float(bk.s
 _WARM_CPU = "print(sum(range(1000)))\n"
 
 
-async def _self_warm(targets: List[str], total: int, concurrency: int, gpu: bool) -> int:
+async def _self_warm(targets: List[str], total: int, concurrency: int, gpu: bool, max_s: float = 30.0) -> int:
     """``total`` Executes through the replicas' own ports, ``concurrency``
-    at a time (closed loop), before the service says it is ready; returns how
-    many completed.  Failures only end the warm-up early."""
+    at a time (closed loop), for at most ``max_s`` seconds, before the
+    service says it is ready; returns how many completed.  Failures only end
+    the warm-up early."""
     import grpc
 
     from .models import proto as pb
@@ -139,9 +140,11 @@ async def _self_warm(targets: List[str], total: int, concurrency: int, gpu: bool
     budget, done = [total], [0]
     src = _WARM_GPU if gpu else _WARM_CPU
 
+    deadline = time.monotonic() + max_s
+
     async def client(i: int) -> None:
         stub = stubs[i % len(stubs)]
-        while budget[0] > 0:
+        while budget[0] > 0 and time.monotonic() < deadline:
             budget[0] -= 1
             try:
                 r = await stub.Execute(pb.ExecuteRequest(source_code=src), timeout=120)
@@ -222,7 +225,7 @@ async def supervise(config: Config, n_frontends: int) -> None:
         t = time.perf_counter()
         n_slots = max(1, len(getattr(backend, "slots", None) or [None]))
         done = await _self_warm(replicas, config.startup_self_warm_executions * n_slots, 8 * n_slots,
-                                gpu=bool(getattr(backend, "gpu_ids", None)))
+                                gpu=bool(getattr(backend, "gpu_ids", None)), max_s=config.startup_self_warm_max_s)
         logger.info("self-warm: %d Executes through %d replicas in %.2f s", done, len(replicas), time.perf_counter() - t)
     print(
         f"BEE_SERVICE_READY grpc={ghost}:{gport} http={hhost}:{hport} frontends={n_frontends} "

@@ -124,6 +124,8 @@ class Config:
     # Executes (the replicas' Python, the daemon's and broker's heaps, the
     # kernel's caches for the fork/exit path grow on first use); 0 = off
     startup_self_warm_executions: int = 3072
+    # ... for at most this many seconds (a CPU-starved node stops early)
+    startup_self_warm_max_s: float = 30.0
     # default execution timeout in seconds (reference: 60 s, `server.rs:201`)
     default_timeout: float = 60.0
     # where sandboxes (workspace + runtime-packages + logs) are created
