@@ -30,6 +30,34 @@ def test_single_process_multi_gpu_run_scales_offered_load():
     assert {"metric", "value", "unit", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling"} <= set(out)
 
 
+def test_torchrun_two_ranks_one_json_line():
+    """The driver's N>1 launch (``torch.distributed.run --nproc-per-node N
+    ... bench.py --gpus N``): rank 0 starts the service, every rank drives
+    its own clients, the timed window is the max over ranks, and only rank 0
+    prints -- one JSON line with the whole job's aggregate."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = subprocess.run(
+        [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+         "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--virtual-gpus", "--workload", "hello",
+         "--steps", "4", "--warmup", "1", "--concurrency", "3", "--no-gang-check"],
+        cwd=ROOT, env=env, capture_output=True, text=True, timeout=600,
+    )
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [line for line in p.stdout.splitlines() if line.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["errors"] == 0 and out["completed"] == 2 * 3 * 4, out
+    assert out["steps"] == 4 and out["warmup"] == 1 and out["scaling"] == "weak"
+    assert abs(out["value"] - out["completed"] / (out["ms_per_step"] * out["steps"] / 1e3)) < 0.05 * out["value"]
+
+
 def _bf16(x):
     """Round float32 to bfloat16 (nearest even), back as float32."""
     import numpy as np
