@@ -502,6 +502,10 @@ def executor_stats(hport):
             d["daemon_cpu_ms_per_exec"] = {k: round(v / n, 3) for k, v in (e.get("cpu_ms") or {}).items()}
             # whole daemon lifetime (start-up included) by thread role
             d["daemon_thread_cpu_ms_per_exec"] = {k: round(v / n, 3) for k, v in (e.get("thread_cpu_ms") or {}).items()}
+            # an executed sandbox's whole CPU (wait4 in its zygote) vs its own
+            # last report: the difference is its teardown (exit, kill)
+            sb = e.get("sandbox_cpu") or {}
+            d["sandbox_cpu"] = {k: round(v, 3) if isinstance(v, float) else v for k, v in sb.items()}
             out.append(d)
         return out
     except Exception as e:  # noqa: BLE001

@@ -512,6 +512,11 @@ void SandboxPool::zygote_reader(Zygote* z) {
         w->quota_cell->store(-1);
         w->term_signal = sig;
         w->exit_code = sig ? -1 : (int)m["code"].as_int();
+        if (m["cpu_us"].is_number() && w->t_run > 0) {  // a sandbox that ran a job: its whole CPU, teardown included
+          m_sb_cpu_us_ += (int64_t)m["cpu_us"].as_number();
+          m_sb_minflt_ += (int64_t)m["minflt"].as_number();
+          m_sb_reaped_++;
+        }
         WorkerState prev = w->state;
         w->state = WorkerState::Exited;
         if (prev == WorkerState::Spawning || prev == WorkerState::Connected) {
@@ -1740,7 +1745,11 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
         if (lead_t_exit > 0) timings.set("w_reap", lead_t_exit - ex);
       }
       // the sandbox process's own CPU (fork to exit, before teardown)
-      if (st["cpu_ms"].is_number()) timings.set("w_cpu", st["cpu_ms"].as_number());
+      if (st["cpu_ms"].is_number()) {
+        timings.set("w_cpu", st["cpu_ms"].as_number());
+        m_sb_wcpu_us_ += (int64_t)(st["cpu_ms"].as_number() * 1e3);
+        m_sb_wcpu_n_++;
+      }
       if (st["minflt"].is_number()) timings.set("w_minflt", st["minflt"].as_number());
       // of which spent while waiting in the pool (warm-up, prefault): off the request path
       if (st["cpu_pool_ms"].is_number()) timings.set("w_cpu_pool", st["cpu_pool_ms"].as_number());
@@ -1789,6 +1798,19 @@ Json SandboxPool::status() {
   j.set("light_target", target_of(kLight));
   j.set("min_target", target_of(kMin));
   j.set("min_cpu_target", target_of(kMinCpu));
+  {
+    // per executed sandbox: its whole CPU (the zygote's wait4, teardown
+    // included) against what it reported itself before exiting
+    Json sb = Json::object();
+    const int64_t n = m_sb_reaped_.load(), nw = m_sb_wcpu_n_.load();
+    const double total = n ? m_sb_cpu_us_.load() / 1e3 / n : 0.0, own = nw ? m_sb_wcpu_us_.load() / 1e3 / nw : 0.0;
+    sb.set("reaped", n);
+    sb.set("cpu_ms_mean", total);
+    sb.set("reported_cpu_ms_mean", own);
+    sb.set("teardown_cpu_ms_mean", n && nw ? total - own : 0.0);
+    sb.set("minflt_mean", n ? (double)m_sb_minflt_.load() / n : 0.0);
+    j.set("sandbox_cpu", sb);
+  }
   Json cpu = Json::object();
   for (int i = 0; i < kCpuParts; ++i) cpu.set(kCpuPartNames[i], g_cpu_ns[i].load() / 1e6);
   j.set("cpu_ms", cpu);

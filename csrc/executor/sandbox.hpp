@@ -276,6 +276,8 @@ class SandboxPool {
   std::vector<std::pair<std::string, int>> cleanup_leaves_;  // (leaf, tries) to remove (under mu_)
   std::string cg_why_;                      // why they are off
   std::atomic<int64_t> m_cg_leaves_{0}, m_cg_oom_kills_{0};
+  // executed sandboxes' CPU: wait4 totals (zygote exit reports) and their own reports
+  std::atomic<int64_t> m_sb_cpu_us_{0}, m_sb_minflt_{0}, m_sb_reaped_{0}, m_sb_wcpu_us_{0}, m_sb_wcpu_n_{0};
   std::vector<gid_t> dev_groups_;          // supplementary groups for GPU device nodes
   std::map<uid_t, int> uids_in_use_;       // UID -> live workers using it (gang ranks share one)
   std::deque<uid_t> uid_sweep_;            // released UIDs awaiting their sweep (cleanup thread)

@@ -707,7 +707,8 @@ PyObject* serve(PyObject*, PyObject* args) {
     int reaped = 0;
     while (true) {
       int status = 0;
-      const pid_t pid = waitpid(-1, &status, WNOHANG);
+      struct rusage ru {};
+      const pid_t pid = wait4(-1, &status, WNOHANG, &ru);
       if (pid <= 0) break;
       ++reaped;
       if (!children.erase(pid)) continue;  // an orphan re-parented here
@@ -716,6 +717,11 @@ PyObject* serve(PyObject*, PyObject* args) {
         m += ",\"code\":-1,\"signal\":" + std::to_string(WTERMSIG(status));
       else
         m += ",\"code\":" + std::to_string(WEXITSTATUS(status)) + ",\"signal\":0";
+      // the sandbox leader's whole CPU, teardown included (what its own
+      // last getrusage cannot see), and its reaped children's
+      const long cpu_us = ru.ru_utime.tv_sec * 1000000L + ru.ru_utime.tv_usec + ru.ru_stime.tv_sec * 1000000L +
+                          ru.ru_stime.tv_usec;
+      m += ",\"cpu_us\":" + std::to_string(cpu_us) + ",\"minflt\":" + std::to_string(ru.ru_minflt);
       write_all(chan, m + "}\n");
     }
     if (reaped && mono_s() - last_sweep >= 0.2) {
