@@ -107,6 +107,29 @@ enum : int {
   // fragments (2p, 2p+1) -- the epilogue stores straight from the
   // accumulators, 16 B per lane, with no LDS staging (epilogue_rows)
   kSwapAB = 32768,
+  // the waves on odd SIMDs (HW_ID) run the ktile_asm schedule with each
+  // group's LDS/VMEM ops ahead of its 4 MFMAs instead of behind them, so the
+  // 4 waves of a CU do not issue their reads and loads in lockstep
+  // (hipBLASLt's MT256x256x64 loop has two such orderings, picked the same way)
+  kAltSimd = 65536,
+  // DIAGNOSTIC (lab only, C overwritten): s_memtime stamps around each
+  // K-tile's wait + barrier; every wave writes (loop cycles, cycles in the
+  // wait + barrier, K-tiles) as 3 u32 at C + 16 * (block * 4 + wave) bytes
+  kDiagStamps = 131072,
+  // DIAGNOSTIC (lab only, wrong C): the K-loop issues no glds (the LDS keeps
+  // the prologue's two tiles): what the loads cost the MFMA stream
+  kDiagNoGlds = 262144,
+  // ktile_asm's second k-half: the 16 glds in groups 0-7 (2 each) and the
+  // 16 next-tile fragment reads in groups 8-15 (2 each), never in one group
+  kSplitGlds = 524288,
+  // every group's memory ops pinned between its MFMAs, apart from each
+  // other: first k-half M M r M M, second k-half M G M M r M (hipBLASLt's
+  // spacing of LDS-DMA loads and LDS reads)
+  kSpacedMem = 1048576,
+};
+// (the stamps' running total while a kDiagStamps kernel runs: one per wave)
+struct StampAcc {
+  uint64_t wait = 0;
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
@@ -379,22 +402,37 @@ __device__ __forceinline__ void glds_one(const Panel& p, int k0, uint16_t* lds_o
 // A ds_read overwrites a fragment register >= 16 MFMAs after its last reader
 // (WAR on srcA/B of an in-flight MFMA, invisible to the hazard recognizer
 // through inline asm).
-template <bool INIT, bool EARLY, bool READS_EARLY, bool KT = false, bool NN = false, bool SW = false>
+template <bool INIT, bool EARLY, bool READS_EARLY, bool KT = false, bool NN = false, bool SW = false,
+          bool ALT = false, bool STAMP = false, bool NOGLDS = false, bool SPLIT = false, bool SPACED = false>
 __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8], bf16x8 (&fa1)[8],
                                           bf16x8 (&fb1)[8], uint16_t* smem, const Panel& pa, const Panel& pb, int t,
-                                          int nk, int wr, int wc, int lane, int wave) {
+                                          int nk, int wr, int wc, int lane, int wave, StampAcc* sa = nullptr) {
   uint16_t* cur = smem + (t & 1) * kBuf;
   uint16_t* nxt = smem + ((t & 1) ^ 1) * kBuf;
   const int rl = lane & 15, ch = lane >> 4;
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
+    auto mfmas = [&]() {
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) mfma_ab<INIT, SW>(acc[g >> 1][(g & 1) * 4 + jj], fa0[g >> 1], fb0[(g & 1) * 4 + jj]);
+      for (int jj = 0; jj < 4; ++jj) mfma_ab<INIT, SW>(acc[g >> 1][(g & 1) * 4 + jj], fa0[g >> 1], fb0[(g & 1) * 4 + jj]);
+    };
     auto read1 = [&](int i) {  // i-th of the 16 k-half-1 fragments: fa1[0..7], fb1[0..7]
       if (i < 8) fa1[i] = frag(cur, wr * 128 + i * 16 + rl, 4 + ch);
       else fb1[i - 8] = fragB(cur + kOperand, wc, i - 8, 1, lane, NN, SW);
     };
+    if constexpr (SPACED && !READS_EARLY) {
+      mfma_ab<INIT, SW>(acc[g >> 1][(g & 1) * 4 + 0], fa0[g >> 1], fb0[(g & 1) * 4 + 0]);
+      mfma_ab<INIT, SW>(acc[g >> 1][(g & 1) * 4 + 1], fa0[g >> 1], fb0[(g & 1) * 4 + 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      read1(g);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_ab<INIT, SW>(acc[g >> 1][(g & 1) * 4 + 2], fa0[g >> 1], fb0[(g & 1) * 4 + 2]);
+      mfma_ab<INIT, SW>(acc[g >> 1][(g & 1) * 4 + 3], fa0[g >> 1], fb0[(g & 1) * 4 + 3]);
+      __builtin_amdgcn_sched_barrier(0);
+      continue;
+    }
+    if constexpr (!ALT) mfmas();
     if constexpr (READS_EARLY) {
       // all 16 reads by group 11 (2 per group in 0..3): the lgkmcnt(0) before
       // the barrier then has 16 MFMAs to cover the last read's latency
@@ -407,16 +445,55 @@ __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], 
     } else {
       read1(g);
     }
+    if constexpr (ALT) {
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas();
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
+  uint64_t ts0 = 0;
+  if constexpr (STAMP) ts0 = __builtin_amdgcn_s_memtime();
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   barrier();
+  if constexpr (STAMP) {
+    const uint64_t ts1 = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    sa->wait += ts1 - ts0;
+  }
   const int kn = min(t + 2, nk - 1) * TK;
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
+    auto mfmas = [&]() {
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) mfma_ab<false, SW>(acc[g >> 1][(g & 1) * 4 + jj], fa1[g >> 1], fb1[(g & 1) * 4 + jj]);
-    if constexpr (EARLY) {  // all 16 glds in the first 8 groups: more time to land
+      for (int jj = 0; jj < 4; ++jj) mfma_ab<false, SW>(acc[g >> 1][(g & 1) * 4 + jj], fa1[g >> 1], fb1[(g & 1) * 4 + jj]);
+    };
+    if constexpr (SPACED && !EARLY && !NOGLDS && !SPLIT) {
+      auto m1 = [&](int jj) { mfma_ab<false, SW>(acc[g >> 1][(g & 1) * 4 + jj], fa1[g >> 1], fb1[(g & 1) * 4 + jj]); };
+      m1(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (g < 8) {
+        if constexpr (NN) glds_a_raw(pa, kn, cur, wave, g);
+        else glds_one(pa, kn, cur, wave, g, KT);
+      } else if constexpr (NN) {
+        glds_nn(pb, kn, cur + kOperand, wave, g - 8);
+      } else {
+        glds_one(pb, kn, cur + kOperand, wave, g - 8, KT);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      m1(1);
+      m1(2);
+      __builtin_amdgcn_sched_barrier(0);
+      if (g == 0) fa0[0] = frag(nxt, wr * 128 + rl, ch);
+      else if (g <= 8) fb0[g - 1] = fragB(nxt + kOperand, wc, g - 1, 0, lane, NN, SW);
+      else fa0[g - 8] = frag(nxt, wr * 128 + (g - 8) * 16 + rl, ch);
+      __builtin_amdgcn_sched_barrier(0);
+      m1(3);
+      __builtin_amdgcn_sched_barrier(0);
+      continue;
+    }
+    if constexpr (!ALT) mfmas();
+    if constexpr (NOGLDS) {
+    } else if constexpr (EARLY || SPLIT) {  // all 16 glds in the first 8 groups: more time to land
       if (g < 8) {
         if constexpr (NN) glds_a_raw(pa, kn, cur, wave, g);
         else glds_one(pa, kn, cur, wave, g, KT);
@@ -433,9 +510,23 @@ __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], 
     }
     // in the order the next K-tile's first groups consume them: fa0[0],
     // fb0[0..7], fa0[1..7]
-    if (g == 0) fa0[0] = frag(nxt, wr * 128 + rl, ch);
-    else if (g <= 8) fb0[g - 1] = fragB(nxt + kOperand, wc, g - 1, 0, lane, NN, SW);
-    else fa0[g - 8] = frag(nxt, wr * 128 + (g - 8) * 16 + rl, ch);
+    auto read0 = [&](int i) {
+      if (i == 0) fa0[0] = frag(nxt, wr * 128 + rl, ch);
+      else if (i <= 8) fb0[i - 1] = fragB(nxt + kOperand, wc, i - 1, 0, lane, NN, SW);
+      else fa0[i - 8] = frag(nxt, wr * 128 + (i - 8) * 16 + rl, ch);
+    };
+    if constexpr (SPLIT) {
+      if (g >= 8) {
+        read0(2 * (g - 8));
+        read0(2 * (g - 8) + 1);
+      }
+    } else {
+      read0(g);
+    }
+    if constexpr (ALT) {
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas();
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -756,13 +847,57 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
     ktile_asm3<true, edge, nn, spread>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
     for (int t = 1; t < nk; ++t)
       ktile_asm3<false, edge, nn, spread>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
+  } else if constexpr (am && inter && (O & kAltSimd) != 0) {
+    read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn, sw);
+    // HW_ID bit 4 = the SIMD's parity (s_getreg_b32 hwreg(HW_REG_HW_ID, 4, 1))
+    if (__builtin_amdgcn_s_getreg((0 << 11) | (4 << 6) | 4) & 1) {
+      ktile_asm<true, early, reads_early, edge, nn, sw, true>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
+      for (int t = 1; t < nk; ++t)
+        ktile_asm<false, early, reads_early, edge, nn, sw, true>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
+    } else {
+      ktile_asm<true, early, reads_early, edge, nn, sw>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
+      for (int t = 1; t < nk; ++t)
+        ktile_asm<false, early, reads_early, edge, nn, sw>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
+    }
+  } else if constexpr (am && inter && (O & kDiagStamps) != 0) {
+    StampAcc sa;
+    read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn, sw);
+    const uint64_t tl0 = __builtin_amdgcn_s_memtime();
+    constexpr bool nog = (O & kDiagNoGlds) != 0, spl = (O & kSplitGlds) != 0, spc = (O & kSpacedMem) != 0;
+    ktile_asm<true, early, reads_early, edge, nn, sw, false, true, nog, spl, spc>(acc, fa0, fb0, fa1, fb1, smem, pa, pb,
+                                                                                  0, nk, wr, wc, lane, wave, &sa);
+    for (int t = 1; t < nk; ++t)
+      ktile_asm<false, early, reads_early, edge, nn, sw, false, true, nog, spl, spc>(acc, fa0, fb0, fa1, fb1, smem, pa,
+                                                                                     pb, t, nk, wr, wc, lane, wave, &sa);
+    const uint64_t tl1 = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    barrier();
+    if constexpr (am) mfma_drain();
+    // the accumulators must stay live (the MFMAs are not volatile): fold
+    // them into one value nobody reads back as data
+    float keep = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) keep += acc[i][j][0] + acc[i][j][3];
+    if (lane == 0) {
+      uint32_t* st = reinterpret_cast<uint32_t*>((char*)C + 16 * ((size_t)blockIdx.x * 4 + wave));
+      st[0] = (uint32_t)(tl1 - tl0);
+      st[1] = (uint32_t)sa.wait;
+      st[2] = (uint32_t)nk;
+      st[3] = __float_as_uint(keep);
+    }
+    return;
   } else if constexpr (am && inter) {
     // hand-interleaved pipeline; K-tile 0 peeled so its MFMAs start the
     // accumulators from the constant 0 (no AGPR zero-fill to fence)
+    constexpr bool nog = (O & kDiagNoGlds) != 0, spl = (O & kSplitGlds) != 0, spc = (O & kSpacedMem) != 0;
     read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn, sw);
-    ktile_asm<true, early, reads_early, edge, nn, sw>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
+    ktile_asm<true, early, reads_early, edge, nn, sw, false, false, nog, spl, spc>(acc, fa0, fb0, fa1, fb1, smem, pa,
+                                                                                   pb, 0, nk, wr, wc, lane, wave);
     for (int t = 1; t < nk; ++t)
-      ktile_asm<false, early, reads_early, edge, nn, sw>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
+      ktile_asm<false, early, reads_early, edge, nn, sw, false, false, nog, spl, spc>(acc, fa0, fb0, fa1, fb1, smem,
+                                                                                      pa, pb, t, nk, wr, wc, lane, wave);
   } else if constexpr ((O & kNoCarry) != 0) {
     // loop-carried state is the accumulators only (simpler register
     // allocation); the first MFMAs of each K-tile wait for its first reads

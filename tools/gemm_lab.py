@@ -27,8 +27,11 @@ NAMES = {0: "round1", 1: "keep_b0", 2: "round1_nostagger", 3: "keep_b0_nostagger
          19: "w4_asm_3bar", 20: "w4_asm_3bar_group8", 21: "w4_asm_3bar_edge",
          22: "w4_asm_3bar_spread", 23: "w4_asm_3bar_spread_edge",
          24: "w4_asm_directstore", 25: "diag_w4_asm_no_epilogue",
-         26: "w4_asm_swapab", 27: "w4_asm_swapab_edge", 28: "diag_w4_asm_swapab_no_epilogue"}
-DIAG = {4, 5, 25, 28}
+         26: "w4_asm_swapab", 27: "w4_asm_swapab_edge", 28: "diag_w4_asm_swapab_no_epilogue",
+         29: "w4_asm_altsimd", 30: "w4_asm_altsimd_swapab", 31: "w4_asm_altsimd_early", 32: "diag_w4_asm_stamps", 33: "diag_w4_asm_stamps_noglds",
+         34: "diag_w4_asm_stamps_split", 35: "w4_asm_splitglds", 36: "diag_w4_asm_noglds",
+         37: "w4_asm_spaced", 38: "diag_w4_asm_stamps_spaced"}
+DIAG = {4, 5, 25, 28, 32, 33, 34, 36, 38}
 PROD = None
 
 
@@ -104,6 +107,7 @@ def main():
     p.add_argument("--repeats", type=int, default=8)
     p.add_argument("--variants", type=int, nargs="*", default=None)
     p.add_argument("--no-check", action="store_true")
+    p.add_argument("--stamps", action="store_true", help="kDiagStamps: cycles per K-tile and in its wait + barrier")
     p.add_argument("--one", type=int, default=None, help="only run this variant (-1 = hipBLASLt) --reps times at 4096^3 (rocprofv3 passes)")
     args = p.parse_args()
     torch.cuda.init()
@@ -116,6 +120,24 @@ def main():
         PROD = _native.lib()
     except Exception:  # noqa: BLE001
         PROD = None
+    if args.stamps:
+        # kDiagStamps: per wave (loop cycles, cycles in the K-tile wait + barrier, K-tiles)
+        for v, size in [(v, size) for v in (32, 33, 38) for size in (4096, 8192)]:
+            a = torch.empty(size, size, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
+            bt = torch.empty(size, size, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
+            c = torch.zeros(size, size, device="cuda", dtype=torch.float32)
+            for _ in range(5):
+                run(lib, v, a, bt, c)
+            torch.cuda.synchronize()
+            nb = (size // 256) ** 2
+            st = c.view(torch.int32).flatten()[: nb * 4 * 4].view(nb * 4, 4).cpu().numpy().astype("int64")
+            loop, wait, nk = st[:, 0] & 0xFFFFFFFF, st[:, 1] & 0xFFFFFFFF, st[:, 2]
+            print(json.dumps({"stamps": size, "variant": NAMES[v], "waves": int(len(loop)), "k_tiles": int(nk[0]),
+                              "loop_cycles_per_ktile_median": float(statistics.median(loop / nk)),
+                              "wait_barrier_cycles_per_ktile_median": float(statistics.median(wait / nk)),
+                              "wait_fraction_median": float(statistics.median(wait / loop)),
+                              "wait_fraction_p90": float(sorted(wait / loop)[int(0.9 * len(loop))])}), flush=True)
+        return
     if args.one is not None:
         a = torch.empty(4096, 4096, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         bt = torch.empty(4096, 4096, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)

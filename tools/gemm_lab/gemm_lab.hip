@@ -40,7 +40,17 @@ constexpr int kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave, g4::kNoCarry, g4::
                            g4::kAsmMfma | g4::kInterleave | g4::kDiagNoEpilogue,
                            g4::kAsmMfma | g4::kInterleave | g4::kSwapAB,
                            g4::kAsmMfma | g4::kInterleave | g4::kSwapAB | g4::kEdge,
-                           g4::kAsmMfma | g4::kInterleave | g4::kSwapAB | g4::kDiagNoEpilogue};
+                           g4::kAsmMfma | g4::kInterleave | g4::kSwapAB | g4::kDiagNoEpilogue,
+                           g4::kAsmMfma | g4::kInterleave | g4::kAltSimd,
+                           g4::kAsmMfma | g4::kInterleave | g4::kAltSimd | g4::kSwapAB,
+                           g4::kAsmMfma | g4::kInterleave | g4::kAltSimd | g4::kEarlyGlds,
+                           g4::kAsmMfma | g4::kInterleave | g4::kDiagStamps,
+                           g4::kAsmMfma | g4::kInterleave | g4::kDiagStamps | g4::kDiagNoGlds,
+                           g4::kAsmMfma | g4::kInterleave | g4::kDiagStamps | g4::kSplitGlds,
+                           g4::kAsmMfma | g4::kInterleave | g4::kSplitGlds,
+                           g4::kAsmMfma | g4::kInterleave | g4::kDiagNoGlds,
+                           g4::kAsmMfma | g4::kInterleave | g4::kSpacedMem,
+                           g4::kAsmMfma | g4::kInterleave | g4::kDiagStamps | g4::kSpacedMem};
 template <int I>
 void run_w4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool bf,
             hipStream_t s) {
@@ -83,6 +93,16 @@ BK_API int gemmlab_run(int variant, const void* A, const void* Bt, void* C, int 
     case 26: run_w4<20>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 27: run_w4<21>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 28: run_w4<22>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 29: run_w4<23>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 30: run_w4<24>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 31: run_w4<25>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 32: run_w4<26>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 33: run_w4<27>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 34: run_w4<28>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 35: run_w4<29>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 36: run_w4<30>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 37: run_w4<31>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 38: run_w4<32>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     default: return kBadArgument;
   }
   return launch_status();
