@@ -129,7 +129,7 @@ enum : int {
 };
 // (the stamps' running total while a kDiagStamps kernel runs: one per wave)
 struct StampAcc {
-  uint64_t wait = 0;
+  uint64_t wait = 0, h0 = 0, h1 = 0, t_end = 0;  // wait + barrier, k-half 0, k-half 1 (to the next K-tile's start)
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
@@ -410,6 +410,11 @@ __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], 
   uint16_t* cur = smem + (t & 1) * kBuf;
   uint16_t* nxt = smem + ((t & 1) ^ 1) * kBuf;
   const int rl = lane & 15, ch = lane >> 4;
+  uint64_t tstart = 0;
+  if constexpr (STAMP) {
+    tstart = __builtin_amdgcn_s_memtime();
+    if (sa->t_end) sa->h1 += tstart - sa->t_end;  // the previous K-tile's second half ends here
+  }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
@@ -459,6 +464,8 @@ __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], 
     const uint64_t ts1 = __builtin_amdgcn_s_memtime();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     sa->wait += ts1 - ts0;
+    sa->h0 += ts0 - tstart;
+    sa->t_end = ts1;
   }
   const int kn = min(t + 2, nk - 1) * TK;
 #pragma unroll
@@ -884,8 +891,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
       uint32_t* st = reinterpret_cast<uint32_t*>((char*)C + 16 * ((size_t)blockIdx.x * 4 + wave));
       st[0] = (uint32_t)(tl1 - tl0);
       st[1] = (uint32_t)sa.wait;
-      st[2] = (uint32_t)nk;
-      st[3] = __float_as_uint(keep);
+      st[2] = (uint32_t)sa.h0 | ((uint32_t)nk << 24);  // h0 < 2^24 cycles at these sizes; nk < 256
+      st[3] = (uint32_t)(sa.h1 + (tl1 - sa.t_end)) ^ (__float_as_uint(keep) & 1u);  // (the last half-1 ends at tl1)
     }
     return;
   } else if constexpr (am && inter) {

@@ -12,7 +12,11 @@
 namespace bk {
 
 constexpr int kShipped = g256::kOptRound1;
-constexpr int kShippedW4 = g4::kAsmMfma | g4::kInterleave;
+// kSpacedMem: each group's LDS-DMA load and LDS read pinned apart between its
+// MFMAs (M G M M r M); s_memtime stamps: the second k-half 1366-1384 vs
+// 1408-1427 cycles per K-tile, 1417 vs 1373 TFLOP/s at 4096^3
+// (profiles/r3_gemm_lab_spaced.log)
+constexpr int kShippedW4 = g4::kAsmMfma | g4::kInterleave | g4::kSpacedMem;
 constexpr int kW4MinK = 256;
 
 bool gemm256_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16) {

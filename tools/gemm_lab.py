@@ -30,7 +30,7 @@ NAMES = {0: "round1", 1: "keep_b0", 2: "round1_nostagger", 3: "keep_b0_nostagger
          26: "w4_asm_swapab", 27: "w4_asm_swapab_edge", 28: "diag_w4_asm_swapab_no_epilogue",
          29: "w4_asm_altsimd", 30: "w4_asm_altsimd_swapab", 31: "w4_asm_altsimd_early", 32: "diag_w4_asm_stamps", 33: "diag_w4_asm_stamps_noglds",
          34: "diag_w4_asm_stamps_split", 35: "w4_asm_splitglds", 36: "diag_w4_asm_noglds",
-         37: "w4_asm_spaced", 38: "diag_w4_asm_stamps_spaced"}
+         37: "w4_asm_spaced", 38: "diag_w4_asm_stamps_spaced", 39: "w4_asm_spaced_edge"}
 DIAG = {4, 5, 25, 28, 32, 33, 34, 36, 38}
 PROD = None
 
@@ -131,12 +131,15 @@ def main():
             torch.cuda.synchronize()
             nb = (size // 256) ** 2
             st = c.view(torch.int32).flatten()[: nb * 4 * 4].view(nb * 4, 4).cpu().numpy().astype("int64")
-            loop, wait, nk = st[:, 0] & 0xFFFFFFFF, st[:, 1] & 0xFFFFFFFF, st[:, 2]
+            loop, wait = st[:, 0] & 0xFFFFFFFF, st[:, 1] & 0xFFFFFFFF
+            h0, nk, h1 = st[:, 2] & 0xFFFFFF, (st[:, 2] >> 24) & 0xFF, st[:, 3] & 0xFFFFFFFF
             print(json.dumps({"stamps": size, "variant": NAMES[v], "waves": int(len(loop)), "k_tiles": int(nk[0]),
                               "loop_cycles_per_ktile_median": float(statistics.median(loop / nk)),
                               "wait_barrier_cycles_per_ktile_median": float(statistics.median(wait / nk)),
                               "wait_fraction_median": float(statistics.median(wait / loop)),
-                              "wait_fraction_p90": float(sorted(wait / loop)[int(0.9 * len(loop))])}), flush=True)
+                              "wait_fraction_p90": float(sorted(wait / loop)[int(0.9 * len(loop))]),
+                              "half0_cycles_per_ktile_median": float(statistics.median(h0 / nk)),
+                              "half1_cycles_per_ktile_median": float(statistics.median(h1 / nk))}), flush=True)
         return
     if args.one is not None:
         a = torch.empty(4096, 4096, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
