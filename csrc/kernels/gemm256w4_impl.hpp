@@ -126,6 +126,9 @@ enum : int {
   // other: first k-half M M r M M, second k-half M G M M r M (hipBLASLt's
   // spacing of LDS-DMA loads and LDS reads)
   kSpacedMem = 1048576,
+  // DIAGNOSTIC (lab only, wrong C; with kDiagStamps): no LDS reads and no
+  // loads in the K-loop -- the MFMA stream alone
+  kDiagMfmaOnly = 2097152,
 };
 // (the stamps' running total while a kDiagStamps kernel runs: one per wave)
 struct StampAcc {
@@ -403,7 +406,8 @@ __device__ __forceinline__ void glds_one(const Panel& p, int k0, uint16_t* lds_o
 // (WAR on srcA/B of an in-flight MFMA, invisible to the hazard recognizer
 // through inline asm).
 template <bool INIT, bool EARLY, bool READS_EARLY, bool KT = false, bool NN = false, bool SW = false,
-          bool ALT = false, bool STAMP = false, bool NOGLDS = false, bool SPLIT = false, bool SPACED = false>
+          bool ALT = false, bool STAMP = false, bool NOGLDS = false, bool SPLIT = false, bool SPACED = false,
+          bool NOREADS = false>
 __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8], bf16x8 (&fa1)[8],
                                           bf16x8 (&fb1)[8], uint16_t* smem, const Panel& pa, const Panel& pb, int t,
                                           int nk, int wr, int wc, int lane, int wave, StampAcc* sa = nullptr) {
@@ -423,6 +427,7 @@ __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], 
       for (int jj = 0; jj < 4; ++jj) mfma_ab<INIT, SW>(acc[g >> 1][(g & 1) * 4 + jj], fa0[g >> 1], fb0[(g & 1) * 4 + jj]);
     };
     auto read1 = [&](int i) {  // i-th of the 16 k-half-1 fragments: fa1[0..7], fb1[0..7]
+      if constexpr (NOREADS) return;
       if (i < 8) fa1[i] = frag(cur, wr * 128 + i * 16 + rl, 4 + ch);
       else fb1[i - 8] = fragB(cur + kOperand, wc, i - 8, 1, lane, NN, SW);
     };
@@ -518,6 +523,7 @@ __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], 
     // in the order the next K-tile's first groups consume them: fa0[0],
     // fb0[0..7], fa0[1..7]
     auto read0 = [&](int i) {
+      if constexpr (NOREADS) return;
       if (i == 0) fa0[0] = frag(nxt, wr * 128 + rl, ch);
       else if (i <= 8) fb0[i - 1] = fragB(nxt + kOperand, wc, i - 1, 0, lane, NN, SW);
       else fa0[i - 8] = frag(nxt, wr * 128 + (i - 8) * 16 + rl, ch);
@@ -870,12 +876,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
     StampAcc sa;
     read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn, sw);
     const uint64_t tl0 = __builtin_amdgcn_s_memtime();
-    constexpr bool nog = (O & kDiagNoGlds) != 0, spl = (O & kSplitGlds) != 0, spc = (O & kSpacedMem) != 0;
-    ktile_asm<true, early, reads_early, edge, nn, sw, false, true, nog, spl, spc>(acc, fa0, fb0, fa1, fb1, smem, pa, pb,
-                                                                                  0, nk, wr, wc, lane, wave, &sa);
+    constexpr bool nor = (O & kDiagMfmaOnly) != 0;
+    constexpr bool nog = (O & kDiagNoGlds) != 0 || nor, spl = (O & kSplitGlds) != 0, spc = (O & kSpacedMem) != 0;
+    if constexpr (nor) read_frags(smem, wr, wc, lane, 1, fa1, fb1, nn, sw);
+    ktile_asm<true, early, reads_early, edge, nn, sw, false, true, nog, spl, spc, nor>(acc, fa0, fb0, fa1, fb1, smem, pa,
+                                                                                       pb, 0, nk, wr, wc, lane, wave, &sa);
     for (int t = 1; t < nk; ++t)
-      ktile_asm<false, early, reads_early, edge, nn, sw, false, true, nog, spl, spc>(acc, fa0, fb0, fa1, fb1, smem, pa,
-                                                                                     pb, t, nk, wr, wc, lane, wave, &sa);
+      ktile_asm<false, early, reads_early, edge, nn, sw, false, true, nog, spl, spc, nor>(acc, fa0, fb0, fa1, fb1, smem,
+                                                                                          pa, pb, t, nk, wr, wc, lane,
+                                                                                          wave, &sa);
     const uint64_t tl1 = __builtin_amdgcn_s_memtime();
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     barrier();

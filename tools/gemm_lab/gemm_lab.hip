@@ -51,7 +51,8 @@ constexpr int kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave, g4::kNoCarry, g4::
                            g4::kAsmMfma | g4::kInterleave | g4::kDiagNoGlds,
                            g4::kAsmMfma | g4::kInterleave | g4::kSpacedMem,
                            g4::kAsmMfma | g4::kInterleave | g4::kDiagStamps | g4::kSpacedMem,
-                           g4::kAsmMfma | g4::kInterleave | g4::kSpacedMem | g4::kEdge};
+                           g4::kAsmMfma | g4::kInterleave | g4::kSpacedMem | g4::kEdge,
+                           g4::kAsmMfma | g4::kInterleave | g4::kDiagStamps | g4::kDiagMfmaOnly};
 template <int I>
 void run_w4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool bf,
             hipStream_t s) {
@@ -105,6 +106,7 @@ BK_API int gemmlab_run(int variant, const void* A, const void* Bt, void* C, int 
     case 37: run_w4<31>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 38: run_w4<32>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 39: run_w4<33>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 40: run_w4<34>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     default: return kBadArgument;
   }
   return launch_status();
