@@ -259,6 +259,19 @@ async def supervise(config: Config, n_frontends: int) -> None:
 
 
 def run() -> None:
+    prof_dir = os.environ.get("BEE_FRONTEND_PROFILE")
+    if prof_dir and os.environ.get("BEE_FRONTEND_INDEX") is not None:
+        # diagnostics: a front-end replica under cProfile, stats dumped at exit
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
+        try:
+            asyncio.run(main())
+        finally:
+            prof.disable()
+            prof.dump_stats(os.path.join(prof_dir, f"frontend-{os.environ['BEE_FRONTEND_INDEX']}.prof"))
+        return
     asyncio.run(main())
 
 
