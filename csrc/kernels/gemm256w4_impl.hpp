@@ -186,7 +186,13 @@ __device__ __forceinline__ srd4 srd_words(const void* base, uint32_t bytes) {
 __device__ __forceinline__ void glds_raw(const srd4& w, const uint16_t* lds, int voff, int soff) {
   const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(lds_void_ptr)(lds));
   const int so = __builtin_amdgcn_readfirstlane(soff);
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0), "v"(voff), "s"(w), "s"(so)
+  // s_nop 0: an M0 write followed by an LDS-DMA load needs one wait state
+  // (cdna_asm_programming.md §4.1 row 16), which the compiler cannot insert
+  // inside the string.  The SGPR operands come from SALU code (no
+  // v_readfirstlane in the K-loop: checked in the -save-temps .s), so no
+  // VALU-write -> VMEM-read pad is needed ahead of the load.
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0), "v"(voff), "s"(w),
+               "s"(so)
                : "memory", "m0");
 }
 
