@@ -129,6 +129,10 @@ enum : int {
   // DIAGNOSTIC (lab only, wrong C; with kDiagStamps): no LDS reads and no
   // loads in the K-loop -- the MFMA stream alone
   kDiagMfmaOnly = 2097152,
+  // kSpacedMem, TN tile multiples: the K-tile's offset moves into each
+  // panel's buffer descriptor once per K-tile, every load's SGPR offset is
+  // loop-invariant (one SALU fewer per load; hipBLASLt's form)
+  kConstSoff = 4194304,
 };
 // (the stamps' running total while a kDiagStamps kernel runs: one per wave)
 struct StampAcc {
@@ -413,7 +417,7 @@ __device__ __forceinline__ void glds_one(const Panel& p, int k0, uint16_t* lds_o
 // through inline asm).
 template <bool INIT, bool EARLY, bool READS_EARLY, bool KT = false, bool NN = false, bool SW = false,
           bool ALT = false, bool STAMP = false, bool NOGLDS = false, bool SPLIT = false, bool SPACED = false,
-          bool NOREADS = false>
+          bool NOREADS = false, bool CSOFF = false>
 __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8], bf16x8 (&fa1)[8],
                                           bf16x8 (&fb1)[8], uint16_t* smem, const Panel& pa, const Panel& pb, int t,
                                           int nk, int wr, int wc, int lane, int wave, StampAcc* sa = nullptr) {
@@ -489,7 +493,18 @@ __device__ __forceinline__ void ktile_asm(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], 
       auto m1 = [&](int jj) { mfma_ab<false, SW>(acc[g >> 1][(g & 1) * 4 + jj], fa1[g >> 1], fb1[(g & 1) * 4 + jj]); };
       m1(0);
       __builtin_amdgcn_sched_barrier(0);
-      if (g < 8) {
+      if constexpr (CSOFF && !NN && !KT) {
+        // descriptor moved to column kn; the row offsets are loop-invariant
+        const Panel& p = g < 8 ? pa : pb;
+        const int i = g & 7;
+        const uint64_t base = (((uint64_t)p.w.y) << 32 | p.w.x) + (uint64_t)kn * 2;
+        srd4 w = p.w;
+        w.x = (uint32_t)base;
+        w.y = (uint32_t)(base >> 32);
+        w.z = p.w.z - (uint32_t)(kn * 2);
+        glds_raw(w, (g < 8 ? cur : cur + kOperand) + (wave * kGlds + i) * 8 * TK, p.lane_off[i & 1],
+                 (wave * 64 + i * 8) * p.row_bytes);
+      } else if (g < 8) {
         if constexpr (NN) glds_a_raw(pa, kn, cur, wave, g);
         else glds_one(pa, kn, cur, wave, g, KT);
       } else if constexpr (NN) {
@@ -882,15 +897,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
     StampAcc sa;
     read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn, sw);
     const uint64_t tl0 = __builtin_amdgcn_s_memtime();
-    constexpr bool nor = (O & kDiagMfmaOnly) != 0;
+    constexpr bool nor = (O & kDiagMfmaOnly) != 0, cso = (O & kConstSoff) != 0;
     constexpr bool nog = (O & kDiagNoGlds) != 0 || nor, spl = (O & kSplitGlds) != 0, spc = (O & kSpacedMem) != 0;
     if constexpr (nor) read_frags(smem, wr, wc, lane, 1, fa1, fb1, nn, sw);
-    ktile_asm<true, early, reads_early, edge, nn, sw, false, true, nog, spl, spc, nor>(acc, fa0, fb0, fa1, fb1, smem, pa,
-                                                                                       pb, 0, nk, wr, wc, lane, wave, &sa);
+    ktile_asm<true, early, reads_early, edge, nn, sw, false, true, nog, spl, spc, nor, cso>(
+        acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave, &sa);
     for (int t = 1; t < nk; ++t)
-      ktile_asm<false, early, reads_early, edge, nn, sw, false, true, nog, spl, spc, nor>(acc, fa0, fb0, fa1, fb1, smem,
-                                                                                          pa, pb, t, nk, wr, wc, lane,
-                                                                                          wave, &sa);
+      ktile_asm<false, early, reads_early, edge, nn, sw, false, true, nog, spl, spc, nor, cso>(
+          acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave, &sa);
     const uint64_t tl1 = __builtin_amdgcn_s_memtime();
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     barrier();
@@ -913,13 +927,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   } else if constexpr (am && inter) {
     // hand-interleaved pipeline; K-tile 0 peeled so its MFMAs start the
     // accumulators from the constant 0 (no AGPR zero-fill to fence)
-    constexpr bool nog = (O & kDiagNoGlds) != 0, spl = (O & kSplitGlds) != 0, spc = (O & kSpacedMem) != 0;
+    constexpr bool nog = (O & kDiagNoGlds) != 0, spl = (O & kSplitGlds) != 0, spc = (O & kSpacedMem) != 0,
+                   cso = (O & kConstSoff) != 0;
     read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn, sw);
-    ktile_asm<true, early, reads_early, edge, nn, sw, false, false, nog, spl, spc>(acc, fa0, fb0, fa1, fb1, smem, pa,
-                                                                                   pb, 0, nk, wr, wc, lane, wave);
+    ktile_asm<true, early, reads_early, edge, nn, sw, false, false, nog, spl, spc, false, cso>(
+        acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
     for (int t = 1; t < nk; ++t)
-      ktile_asm<false, early, reads_early, edge, nn, sw, false, false, nog, spl, spc>(acc, fa0, fb0, fa1, fb1, smem,
-                                                                                      pa, pb, t, nk, wr, wc, lane, wave);
+      ktile_asm<false, early, reads_early, edge, nn, sw, false, false, nog, spl, spc, false, cso>(
+          acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
   } else if constexpr ((O & kNoCarry) != 0) {
     // loop-carried state is the accumulators only (simpler register
     // allocation); the first MFMAs of each K-tile wait for its first reads

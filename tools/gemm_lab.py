@@ -30,8 +30,9 @@ NAMES = {0: "round1", 1: "keep_b0", 2: "round1_nostagger", 3: "keep_b0_nostagger
          26: "w4_asm_swapab", 27: "w4_asm_swapab_edge", 28: "diag_w4_asm_swapab_no_epilogue",
          29: "w4_asm_altsimd", 30: "w4_asm_altsimd_swapab", 31: "w4_asm_altsimd_early", 32: "diag_w4_asm_stamps", 33: "diag_w4_asm_stamps_noglds",
          34: "diag_w4_asm_stamps_split", 35: "w4_asm_splitglds", 36: "diag_w4_asm_noglds",
-         37: "w4_asm_spaced", 38: "diag_w4_asm_stamps_spaced", 39: "w4_asm_spaced_edge", 40: "diag_w4_asm_stamps_mfma_only"}
-DIAG = {4, 5, 25, 28, 32, 33, 34, 36, 38, 40}
+         37: "w4_asm_spaced", 38: "diag_w4_asm_stamps_spaced", 39: "w4_asm_spaced_edge", 40: "diag_w4_asm_stamps_mfma_only",
+         41: "w4_asm_spaced_csoff", 42: "diag_w4_asm_stamps_spaced_csoff"}
+DIAG = {4, 5, 25, 28, 32, 33, 34, 36, 38, 40, 42}
 PROD = None
 
 
@@ -122,7 +123,7 @@ def main():
         PROD = None
     if args.stamps:
         # kDiagStamps: per wave (loop cycles, cycles in the K-tile wait + barrier, K-tiles)
-        for v, size in [(v, size) for v in (32, 33, 38, 40) for size in (4096,)]:
+        for v, size in [(v, size) for v in (38, 42) for size in (4096, 8192)]:
             a = torch.empty(size, size, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
             bt = torch.empty(size, size, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
             c = torch.zeros(size, size, device="cuda", dtype=torch.float32)

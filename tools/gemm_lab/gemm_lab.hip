@@ -52,7 +52,9 @@ constexpr int kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave, g4::kNoCarry, g4::
                            g4::kAsmMfma | g4::kInterleave | g4::kSpacedMem,
                            g4::kAsmMfma | g4::kInterleave | g4::kDiagStamps | g4::kSpacedMem,
                            g4::kAsmMfma | g4::kInterleave | g4::kSpacedMem | g4::kEdge,
-                           g4::kAsmMfma | g4::kInterleave | g4::kDiagStamps | g4::kDiagMfmaOnly};
+                           g4::kAsmMfma | g4::kInterleave | g4::kDiagStamps | g4::kDiagMfmaOnly,
+                           g4::kAsmMfma | g4::kInterleave | g4::kSpacedMem | g4::kConstSoff,
+                           g4::kAsmMfma | g4::kInterleave | g4::kDiagStamps | g4::kSpacedMem | g4::kConstSoff};
 template <int I>
 void run_w4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool bf,
             hipStream_t s) {
@@ -107,6 +109,8 @@ BK_API int gemmlab_run(int variant, const void* A, const void* Bt, void* C, int 
     case 38: run_w4<32>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 39: run_w4<33>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 40: run_w4<34>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 41: run_w4<35>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 42: run_w4<36>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     default: return kBadArgument;
   }
   return launch_status();
