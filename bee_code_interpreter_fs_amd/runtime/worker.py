@@ -252,18 +252,27 @@ def warm_gpu() -> Optional[str]:
         return f"{type(e).__name__}: {e}"
 
 
-def _run_main(path: str) -> None:
+def _run_main(path: str, lowered: Optional[str] = None) -> None:
     """`python path` semantics (what runpy.run_path does for a plain file,
     minus its zip/directory probing): compile, bind a fresh ``__main__``
-    module, execute.  The module is left alive -- the process ends with
-    os._exit, and the broker releases device memory on disconnect -- so no
-    teardown work lands on the request path."""
-    with io.open_code(path) as fh:
-        source = fh.read()
+    module, execute.  ``lowered``: the payload with its xonsh shell lines
+    lowered to Python (runtime/xsh.py), compiled under the same file name so
+    tracebacks point at the user's lines.  The module is left alive -- the
+    process ends with os._exit, and the broker releases device memory on
+    disconnect -- so no teardown work lands on the request path."""
+    if lowered is None:
+        with io.open_code(path) as fh:
+            source = fh.read()
+    else:
+        source = lowered
     code = compile(source, path, "exec", dont_inherit=True)
     mod = types.ModuleType("__main__")
     mod.__dict__.update({"__file__": path, "__cached__": None, "__loader__": None, "__package__": None,
                          "__spec__": None, "__builtins__": builtins})
+    if lowered is not None:
+        from . import xsh
+
+        mod.__dict__[xsh.RUNTIME_NAME] = xsh.Runtime()
     sys.modules["__main__"] = mod
     try:
         exec(code, mod.__dict__)
@@ -301,18 +310,23 @@ def run_script(script: str, argv, workspace: str, runtime_packages: str) -> int:
     from . import sandbox_patches
 
     sandbox_patches.install()
+    lowered = None
     try:
         with open(script, "rb") as fh:
             source = fh.read().decode("utf-8", errors="replace")
+        from . import xsh
         from .deps import install_missing
 
-        install_missing(source, runtime_packages)
+        # xonsh-style shell lines (the reference ran every payload through
+        # xonsh): lowered to Python here, plain Python passes untouched
+        lowered = xsh.lower_payload(source)
+        install_missing(lowered or source, runtime_packages)
     except OSError:
         pass
     code = 0
     _STAMPS["script_start"] = time.monotonic() * 1e3
     try:
-        _run_main(script)
+        _run_main(script, lowered)
     except SystemExit as e:
         if e.code is None:
             code = 0

@@ -59,7 +59,7 @@ def _preload() -> list:
             pass
     # everything a worker runs before user code, done once here: the sandbox
     # patches are applied pre-fork and inherited by every worker
-    from . import deps, sandbox_patches, worker  # noqa: F401
+    from . import deps, sandbox_patches, worker, xsh  # noqa: F401
 
     # `import beekern` (the sandbox alias of the ops module) resolved pre-fork
     if "bee_code_interpreter_fs_amd.ops" in sys.modules:
