@@ -236,12 +236,15 @@ def gpu_ids(n_gpus: int, args):
 
 def start_service(tmp: str, n_gpus: int, args):
     gport, hport = free_port(), free_port()
-    # three front-end replicas per GPU (at most 16): one Python gRPC process
-    # saturates a core at ~2.2k Execute/s (2235 -> 2378 RPS with a second
-    # replica on one GPU, profiles/archive/r2_bench_frontends_ab.log); a third took
-    # p50 down in 3 of 3 interleaved pairs, 2794 vs 2734 RPS mean
-    # (profiles/archive/r2_s3_frontends3_ab.log)
-    frontends = args.frontends or min(16, 3 * max(1, n_gpus))
+    # three front-end replicas per GPU: one Python gRPC process saturates a
+    # core at ~2.2k Execute/s (2235 -> 2378 RPS with a second replica on one
+    # GPU, profiles/archive/r2_bench_frontends_ab.log); a third took p50 down
+    # in 3 of 3 interleaved pairs, 2794 vs 2734 RPS mean
+    # (profiles/archive/r2_s3_frontends3_ab.log).  The same three per GPU at
+    # every N keeps each replica's share of the offered load (8 clients per
+    # GPU) what it is on one GPU -- weak scaling of the front-end too (24 at
+    # N = 8; front-ends hold no GPU context)
+    frontends = args.frontends or min(32, 3 * max(1, n_gpus))
     env = dict(os.environ)
     env.update(
         {

@@ -136,7 +136,7 @@ def test_front_end_routes_by_the_published_load(node1):
 
 
 def test_eight_gpu_rehearsal_balances_and_holds_the_bounds(tmp_path):
-    """bench.py on 8 virtual GPUs with 16 front-end replicas (the driver's
+    """bench.py on 8 virtual GPUs with 24 front-end replicas (the driver's
     8-GPU topology) and a per-GPU bound of 4 under 8 closed-loop clients per
     GPU: every slot's executions within +-10% of the mean, no daemon ever
     above its bound, impossible requests refused in under a second."""
@@ -150,7 +150,7 @@ def test_eight_gpu_rehearsal_balances_and_holds_the_bounds(tmp_path):
     out = json.loads([line for line in p.stdout.splitlines() if line.startswith("{")][-1])
     assert out["errors"] == 0 and out["completed"] == 8 * 8 * 25, out
     ex = out["executors"]
-    assert len(ex) == 8 and "16 front-end replicas" in out["config"]["parallelism"], out["config"]
+    assert len(ex) == 8 and "24 front-end replicas" in out["config"]["parallelism"], out["config"]
     counts = [e["executions"] for e in ex]
     mean = sum(counts) / len(counts)
     assert all(abs(c - mean) <= 0.10 * mean for c in counts), counts
