@@ -100,6 +100,12 @@ class Config:
     # their kernel-broker session opens only if used (-1 = as many as the
     # minimal pool)
     min_cpu_workers_per_gpu_target: int = -1
+    # warm "nano" sandboxes per GPU: beekern only, forked from zygotes that
+    # never imported numpy (ops/_lazy.py), for scripts whose imports are
+    # beekern + the standard library; 0 = such scripts use minimal sandboxes
+    nano_workers_per_gpu_target: int = 16
+    # zygote processes forking nano sandboxes per GPU
+    nano_zygotes_per_gpu: int = 4
     # run the per-GPU kernel broker in the executor daemon
     broker_enabled: bool = True
     # zygote processes forking light sandboxes per GPU (fork parallelism)

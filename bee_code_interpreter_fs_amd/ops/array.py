@@ -20,11 +20,11 @@ from __future__ import annotations
 
 import math
 import os
+import struct
 import threading
 from typing import Any, Optional, Sequence, Tuple
 
-import numpy as np
-
+from ._lazy import is_integer, is_number, np, scalar
 from ._native import DTYPE_CODES, DTYPE_SIZES, BeekernError, QuotaExceeded  # noqa: F401
 from .driver import make_driver
 
@@ -37,7 +37,6 @@ _UNARY = {
 _BINARY = {"add": 0, "subtract": 1, "multiply": 2, "divide": 3, "maximum": 4, "minimum": 5, "power": 6}
 _REDUCE = {"sum": 0, "square_sum": 1, "abs_sum": 2, "max": 3, "min": 4, "dot": 5, "max_abs_diff": 6}
 _SUPPORTED = ("float32", "float64", "bfloat16")
-_NP_DTYPES = {"float32": np.float32, "float64": np.float64}
 
 _state_lock = threading.Lock()
 _driver = None
@@ -283,8 +282,12 @@ class DeviceArray:
     def __matmul__(self, o): return matmul(self, o)
 
 
+def _np_dtype(dtype: str):
+    return {"float32": np.float32, "float64": np.float64}[dtype]
+
+
 def _np_view_dtype(dtype: str):
-    return np.uint16 if dtype == "bfloat16" else _NP_DTYPES[dtype]
+    return np.uint16 if dtype == "bfloat16" else _np_dtype(dtype)
 
 
 def _download(buf: _Buffer, shape: Shape, dtype: str) -> np.ndarray:
@@ -300,6 +303,14 @@ def _upload(host: np.ndarray, dtype: str) -> _Buffer:
     buf = _Buffer(host.nbytes)
     driver().h2d(buf.ptr, host)
     return buf
+
+
+def _f32_bits_to_bf16(u: int) -> int:
+    """One f32 bit pattern -> bf16 bits, round to nearest even (NaN -> 0x7FC0),
+    as _f32_to_bf16_bits does element-wise."""
+    if (u & 0x7F800000) == 0x7F800000 and (u & 0x007FFFFF):
+        return 0x7FC0
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) & 0xFFFF
 
 
 def _f32_to_bf16_bits(a: np.ndarray) -> np.ndarray:
@@ -321,12 +332,13 @@ def empty(shape, dtype="float64") -> DeviceArray:
 
 def full(shape, value: float, dtype="float64") -> DeviceArray:
     a = empty(shape, dtype)
+    # the fill's bit pattern (no numpy: see ops/_lazy.py)
     if a.dtype == "float64":
-        pattern, width = int(np.array(value, np.float64).view(np.uint64)), 8
+        pattern, width = struct.unpack("<Q", struct.pack("<d", float(value)))[0], 8
     elif a.dtype == "float32":
-        pattern, width = int(np.array(value, np.float32).view(np.uint32)), 4
+        pattern, width = struct.unpack("<I", struct.pack("<f", float(value)))[0], 4
     else:
-        pattern, width = int(_f32_to_bf16_bits(np.array([value], np.float32))[0]), 2
+        pattern, width = _f32_bits_to_bf16(struct.unpack("<I", struct.pack("<f", float(value)))[0]), 2
     driver().fill(a.ptr, a.nbytes, pattern, width)
     return a
 
@@ -349,7 +361,7 @@ def asarray(obj, dtype=None) -> DeviceArray:
     if dt == "bfloat16":
         buf = _upload(_f32_to_bf16_bits(host.astype(np.float32)), "bfloat16")
     else:
-        buf = _upload(host.astype(_NP_DTYPES[dt], copy=False), dt)
+        buf = _upload(host.astype(_np_dtype(dt), copy=False), dt)
     return DeviceArray(host.shape, dt, buffer=buf)
 
 
@@ -410,7 +422,7 @@ def square(x) -> DeviceArray:
 
 def _binary(op: str, a, b, reversed_: bool = False) -> DeviceArray:
     a = _as_operand(a)._materialize()
-    if isinstance(b, (int, float, np.floating, np.integer)):
+    if is_number(b):
         out = DeviceArray(a.shape, a.dtype)
         driver().binary(_BINARY[op], a.code, 2 if reversed_ else 1, a.ptr, 0, float(b), out.ptr, a.size)
         return out
@@ -427,7 +439,7 @@ def _binary(op: str, a, b, reversed_: bool = False) -> DeviceArray:
 
 
 def _reduce(op: str, x: DeviceArray, y: Optional[DeviceArray] = None) -> np.float64:
-    return np.float64(driver().reduce(_REDUCE[op], x.code, x.ptr, y.ptr if y is not None else 0, x.size))
+    return scalar(driver().reduce(_REDUCE[op], x.code, x.ptr, y.ptr if y is not None else 0, x.size))
 
 
 def _lazy_uniform(x: DeviceArray) -> bool:
@@ -439,7 +451,7 @@ def _rand_reduce(op: str, x: DeviceArray) -> np.float64:
     """Reduce a still-lazy uniform draw in one fused Philox->reduce kernel
     (bk_rand_reduce): the values are the ones materialising x would store."""
     _, _, seed, off, lo, hi = x._lazy
-    return np.float64(driver().rand_reduce(_REDUCE[op], x.code, x.size, seed, off, lo, hi))
+    return scalar(driver().rand_reduce(_REDUCE[op], x.code, x.size, seed, off, lo, hi))
 
 
 def _reduce_axis(op: str, x: DeviceArray, axis: int):
@@ -702,7 +714,7 @@ class Generator:
 def _shape_of(size) -> Shape:
     if size is None:
         return (1,)
-    if isinstance(size, (int, np.integer)):
+    if is_integer(size):
         return (int(size),)
     if len(size) == 1 and isinstance(size[0], (tuple, list)):
         return tuple(int(s) for s in size[0])

@@ -24,9 +24,8 @@ import threading
 import time
 from typing import Optional
 
-import numpy as np
-
 from . import _native
+from ._lazy import np
 from ._native import BeekernError, QuotaExceeded, check
 
 _vp = ctypes.c_void_p

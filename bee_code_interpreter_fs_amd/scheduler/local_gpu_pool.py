@@ -231,6 +231,8 @@ class LocalGpuPoolBackend(CodeExecutor):
             extra_args=["--max-idle", str(c.worker_max_idle_s), "--min-target", str(c.min_workers_per_gpu_target),
                         "--min-zygotes", str(c.min_zygotes_per_gpu),
                         "--min-cpu-target", str(c.min_cpu_workers_per_gpu_target),
+                        "--nano-target", str(c.nano_workers_per_gpu_target),
+                        "--nano-zygotes", str(c.nano_zygotes_per_gpu),
                         "--gang-grace", str(c.gang_failure_grace_s),
                         # admission for every front-end replica of the node
                         "--max-inflight", str(max(c.max_inflight_per_gpu, 0)),
@@ -260,7 +262,8 @@ class LocalGpuPoolBackend(CodeExecutor):
                     and st.get("ready_direct", 0) >= st.get("target", 0)
                     and st.get("ready_light", 0) >= st.get("light_target", 0)
                     and st.get("ready_min", 0) >= st.get("min_target", 0)
-                    and st.get("ready_min_cpu", 0) >= st.get("min_cpu_target", 0))
+                    and st.get("ready_min_cpu", 0) >= st.get("min_cpu_target", 0)
+                    and st.get("ready_nano", 0) >= st.get("nano_target", 0))
 
         while loop.time() < deadline:
             try:
@@ -562,6 +565,10 @@ def _mode_of_source(source: str) -> str:
     mods = imported_modules(source)
     if DIRECT_GPU_MODULES.intersection(mods):
         return "direct"
+    if all(m in GPU_API_MODULES or m in _STDLIB for m in mods) and GPU_API_MODULES.intersection(mods):
+        # beekern + stdlib: a sandbox from a zygote that never imported numpy
+        # (executor kind nano; the daemon falls back to a minimal one)
+        return "nano"
     if all(m in MIN_MODULES or m in _STDLIB for m in mods):
         # numpy/beekern/stdlib only: the fast-forking minimal zygote; scripts
         # that never import beekern take a sandbox whose broker session opens

@@ -258,6 +258,8 @@ def start_service(tmp: str, n_gpus: int, args):
             "APP_WORKERS_PER_GPU_TARGET": "1",  # direct sandboxes: the payload does not need them
             # the payloads import only beekern/numpy/stdlib -> minimal sandboxes
             "APP_MIN_WORKERS_PER_GPU_TARGET": str(args.pool_target),
+            # beekern + stdlib payloads (the headline): numpy-free zygotes
+            "APP_NANO_WORKERS_PER_GPU_TARGET": os.environ.get("APP_NANO_WORKERS_PER_GPU_TARGET", str(args.pool_target)),
             # light sandboxes (pandas/scipy/matplotlib preloaded) serve the
             # scientific workload; the others only keep a few warm
             "APP_LIGHT_WORKERS_PER_GPU_TARGET": str(args.pool_target if args.workload == "scientific" else 4),
@@ -275,7 +277,8 @@ def start_service(tmp: str, n_gpus: int, args):
         # each kind per slot), no kernel broker, no HIP warm-up
         env.update({"APP_BROKER_ENABLED": "false", "APP_WORKER_WARM_GPU": "false", "APP_WORKERS_PER_GPU_TARGET": "0",
                     "APP_LIGHT_WORKERS_PER_GPU_TARGET": "1", "APP_LIGHT_ZYGOTES_PER_GPU": "1",
-                    "APP_MIN_ZYGOTES_PER_GPU": "1", "APP_MIN_WORKERS_PER_GPU_TARGET": str(min(args.pool_target, 4))})
+                    "APP_MIN_ZYGOTES_PER_GPU": "1", "APP_MIN_WORKERS_PER_GPU_TARGET": str(min(args.pool_target, 4)),
+                    "APP_NANO_WORKERS_PER_GPU_TARGET": "0"})
     env.pop("RANK", None), env.pop("WORLD_SIZE", None), env.pop("LOCAL_RANK", None)
     log = open(os.path.join(tmp, "service.log"), "ab")
     proc = subprocess.Popen(

@@ -134,6 +134,9 @@ int main(int argc, char** argv) {
     else if (a == "--min-zygotes") cfg.min_zygotes = atoi(val().c_str());
     else if (a == "--min-cpu-target") cfg.min_cpu_target = atoi(val().c_str());
     else if (a == "--min-preload") cfg.min_preload = val();
+    else if (a == "--nano-target") cfg.nano_target = atoi(val().c_str());
+    else if (a == "--nano-zygotes") cfg.nano_zygotes = atoi(val().c_str());
+    else if (a == "--nano-preload") cfg.nano_preload = val();
     else if (a == "--runtime-packages") cfg.pod_runtime_packages = val();
     else if (a == "--cpus") cpus_spec = val();
     else if (a == "--jail") cfg.jail = val() != "0";

@@ -78,6 +78,17 @@ bool user_env_ok(const std::string& k) {
   return true;
 }
 
+const char* kind_name(int kind) {
+  switch (kind) {
+    case kDirect: return "direct";
+    case kLight: return "light";
+    case kMin: return "min";
+    case kMinCpu: return "min_cpu";
+    case kNano: return "nano";
+  }
+  return "?";
+}
+
 const char* state_name(WorkerState s) {
   switch (s) {
     case WorkerState::Spawning: return "spawning";
@@ -186,14 +197,16 @@ bool SandboxPool::start(std::string* err) {
   const bool cpu_light = !want_broker && !cfg_.pod_mode && cfg_.light_target > 0 && cfg_.light_zygotes > 0;
   const int nl = want_broker || cpu_light ? std::max(1, cfg_.light_zygotes) : 0;
   const int nm = nl > 0 && cfg_.min_target > 0 ? cfg_.min_zygotes : 0;
-  for (int i = 0; i < 1 + nl + nm; ++i) {
+  const int nn = nl > 0 && cfg_.nano_target > 0 ? cfg_.nano_zygotes : 0;
+  for (int i = 0; i < 1 + nl + nm + nn; ++i) {
     auto z = std::make_unique<Zygote>();
     z->index = i;
-    z->kind = i == 0 ? kDirect : i <= nl ? kLight : kMin;
+    z->kind = i == 0 ? kDirect : i <= nl ? kLight : i <= nl + nm ? kMin : kNano;
     if (!start_zygote(z.get(), err)) return false;
     zygotes_.push_back(std::move(z));
   }
   min_ok_ = nm > 0;
+  nano_ok_ = nn > 0;
   if (want_broker) {
     broker_ = std::make_unique<KernelBroker>(broker_sock_path_,
                                              cfg_.broker_lib, [this](pid_t p) { return peer_info(p); });
@@ -377,6 +390,7 @@ bool SandboxPool::start_zygote(Zygote* z, std::string* err) {
   if (!cfg_.zygote_preload.empty() && !getenv("BEE_ZYGOTE_THP_EARLY")) env_store.push_back("BEE_ZYGOTE_THP_EARLY=1");
   if (z->kind == kLight) env_store.push_back("BEE_PRELOAD=" + cfg_.light_preload);
   if (z->kind == kMin) env_store.push_back("BEE_PRELOAD=" + cfg_.min_preload);
+  if (z->kind == kNano) env_store.push_back("BEE_PRELOAD=" + cfg_.nano_preload);
   if (!cfg_.pythonpath.empty()) {
     const char* old = getenv("PYTHONPATH");
     env_store.push_back("PYTHONPATH=" + cfg_.pythonpath + (old && *old ? std::string(":") + old : ""));
@@ -426,7 +440,7 @@ bool SandboxPool::start_zygote(Zygote* z, std::string* err) {
   z->alive = true;
   if (z->thread.joinable()) z->thread.detach();
   z->thread = std::thread([this, z] { zygote_reader(z); });
-  BEE_INFO("zygote %d (%s) started pid=%d (%s -m %s), gpus='%s'", z->index, z->kind == kLight ? "light" : z->kind == kMin ? "min" : "direct",
+  BEE_INFO("zygote %d (%s) started pid=%d (%s -m %s), gpus='%s'", z->index, kind_name(z->kind),
            pid, cfg_.python.c_str(), cfg_.zygote_module.c_str(), cfg_.gpus.c_str());
   return true;
 }
@@ -812,6 +826,7 @@ int SandboxPool::target_of(int kind) const {
   if (kind == kLight) return light_ok_ ? cfg_.light_target : 0;
   if (kind == kMin) return light_ok_ && min_ok_ ? cfg_.min_target : 0;
   if (kind == kMinCpu) return broker_ && min_ok_ ? (cfg_.min_cpu_target >= 0 ? cfg_.min_cpu_target : cfg_.min_target) : 0;
+  if (kind == kNano) return light_ok_ && nano_ok_ ? cfg_.nano_target : 0;
   return cfg_.target;
 }
 
@@ -1452,6 +1467,7 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   const int kind = !light_ok_ ? kDirect
                    : mode == "min_cpu" ? (target_of(kMinCpu) > 0 ? kMinCpu : min_ok_ ? kMin : kLight)
                    : mode == "min" ? (min_ok_ ? kMin : kLight)
+                   : mode == "nano" ? (nano_ok_ ? kNano : min_ok_ ? kMin : kLight)
                    : mode == "light" ? kLight
                                      : kDirect;
   if (!dedicated) {
@@ -1798,6 +1814,7 @@ Json SandboxPool::status() {
   j.set("light_target", target_of(kLight));
   j.set("min_target", target_of(kMin));
   j.set("min_cpu_target", target_of(kMinCpu));
+  j.set("nano_target", target_of(kNano));
   {
     // per executed sandbox: its whole CPU (the zygote's wait4, teardown
     // included) against what it reported itself before exiting
@@ -1817,12 +1834,15 @@ Json SandboxPool::status() {
   Json thr = Json::object();
   for (auto& kv : thread_cpu_report()) thr.set(kv.first, kv.second);
   j.set("thread_cpu_ms", thr);
-  j.set("ready", (int64_t)(ready_[kDirect].size() + ready_[kLight].size() + ready_[kMin].size() + ready_[kMinCpu].size()));
+  int64_t ready_all = 0, spawning_all = 0;
+  for (int k = 0; k < kNumKinds; ++k) ready_all += (int64_t)ready_[k].size(), spawning_all += spawning_[k];
+  j.set("ready", ready_all);
+  j.set("ready_nano", (int64_t)ready_[kNano].size());
   j.set("ready_min_cpu", (int64_t)ready_[kMinCpu].size());
   j.set("ready_min", (int64_t)ready_[kMin].size());
   j.set("ready_direct", (int64_t)ready_[kDirect].size());
   j.set("ready_light", (int64_t)ready_[kLight].size());
-  j.set("spawning", spawning_[kDirect] + spawning_[kLight] + spawning_[kMin] + spawning_[kMinCpu]);
+  j.set("spawning", spawning_all);
   if (broker_) {
     Json b = Json::object();
     b.set("arch", broker_->arch());
@@ -1931,13 +1951,14 @@ std::string SandboxPool::metrics_text() {
     s += std::string("bee_executor_cpu_seconds_total{gpus=\"") + cfg_.gpus + "\",part=\"" + kCpuPartNames[i] + "\"} " +
          std::to_string(g_cpu_ns[i].load() / 1e9) + "\n";
   line("bee_executor_inflight", "gauge", (double)m_inflight_.load());
-  line("bee_executor_ready_workers", "gauge",
-       (double)(ready_[kDirect].size() + ready_[kLight].size() + ready_[kMin].size() + ready_[kMinCpu].size()));
+  double ready_all = 0, spawning_all = 0;
+  for (int k = 0; k < kNumKinds; ++k) ready_all += (double)ready_[k].size(), spawning_all += spawning_[k];
+  line("bee_executor_ready_workers", "gauge", ready_all);
+  line("bee_executor_ready_nano_workers", "gauge", (double)ready_[kNano].size());
   line("bee_executor_ready_min_workers", "gauge", (double)ready_[kMin].size());
   line("bee_executor_ready_light_workers", "gauge", (double)ready_[kLight].size());
   line("bee_executor_ready_min_cpu_workers", "gauge", (double)ready_[kMinCpu].size());
-  line("bee_executor_spawning_workers", "gauge",
-       (double)(spawning_[kDirect] + spawning_[kLight] + spawning_[kMin] + spawning_[kMinCpu]));
+  line("bee_executor_spawning_workers", "gauge", spawning_all);
   if (broker_) {
     line("bee_executor_broker_ops_total", "counter", (double)broker_->ops());
     line("bee_executor_broker_live_bytes", "gauge", (double)broker_->live_bytes());

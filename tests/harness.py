@@ -44,6 +44,10 @@ class ServiceHarness:
             gpu_ids=[],
             workers_per_gpu_target=2,
             executor_backend="local",
+            # a small numpy-free pool: enough to serve the tests that route
+            # there, without 16 more sandboxes per service on the CPU runner
+            nano_workers_per_gpu_target=2,
+            nano_zygotes_per_gpu=1,
         )
         base.update(overrides)
         self.config = Config(_env={}, **base)

@@ -372,7 +372,10 @@ def test_sandbox_mode_routing(tmp_path):
     assert mode("print(1)") == "min_cpu"  # no GPU module: lazy broker session
     assert mode("import numpy as np, time, json") == "min_cpu"
     assert mode("import numpy as np, time, json\nimport beekern as bk") == "min"
-    assert mode("from bee_code_interpreter_fs_amd import ops") == "min"
+    assert mode("from bee_code_interpreter_fs_amd import ops") == "nano"
+    assert mode("import time\nimport beekern as bk") == "nano"  # numpy-free zygote
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    assert mode(open(os.path.join(root, "examples", "benchmark_numpy_gpu.py")).read()) == "nano"
     assert mode("import pandas as pd") == "light"
     assert mode("from scipy import stats") == "light"
     assert mode("import torch") == "direct"
@@ -504,3 +507,31 @@ def test_cpu_quota_and_quota_pinning(tmp_path):
     assert t.slot_cpus(0, str(sys_), allowed=set(range(24)), slots=[0], quota=16.0) == []  # quota ~ what may run
     assert t.core_order([0, 128, 1, 129], str(sys_)) == [0, 1, 128, 129]
     assert t.gpu_numa_nodes(str(tmp_path / "missing")) == []
+
+
+def test_beekern_imports_without_numpy_and_fill_patterns_match():
+    """ops/_lazy.py: importing beekern does not import numpy (the nano
+    zygote's premise), and full()'s struct-built fill patterns equal the
+    numpy-built ones (bf16: round to nearest even, NaN -> 0x7FC0)."""
+    import math
+    import struct
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", "import sys; import bee_code_interpreter_fs_amd.ops as o; "
+                          "print('numpy' in sys.modules, o.sum.__module__)"], cwd=root, capture_output=True, text=True)
+    assert out.stdout.split() == ["False", "bee_code_interpreter_fs_amd.ops.array"], out.stderr
+
+    import numpy as np
+
+    from bee_code_interpreter_fs_amd.ops import _lazy
+    from bee_code_interpreter_fs_amd.ops.array import _f32_bits_to_bf16, _f32_to_bf16_bits
+
+    vals = [0.0, -0.0, 1.0, -1.5, 3.14159, 1e-40, 65504.0, 1.00390625, 1.01171875, 3.4e38, math.inf, -math.inf,
+            math.nan, 0.1, -2.71828]
+    ref = _f32_to_bf16_bits(np.array(vals, np.float32))
+    got = [_f32_bits_to_bf16(struct.unpack("<I", struct.pack("<f", v))[0]) for v in vals]
+    assert got == [int(x) for x in ref]
+    assert _lazy.scalar(1.5) == 1.5 and isinstance(_lazy.scalar(1.5), np.float64)  # numpy loaded here
+    assert _lazy.is_number(np.float32(2)) and _lazy.is_integer(np.int64(3)) and not _lazy.is_integer(2.0)
