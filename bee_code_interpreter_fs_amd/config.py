@@ -106,6 +106,9 @@ class Config:
     nano_workers_per_gpu_target: int = 16
     # zygote processes forking nano sandboxes per GPU
     nano_zygotes_per_gpu: int = 4
+    # warm nano sandboxes per GPU for standard-library-only scripts (broker
+    # session opened on first use; -1 = as many as the nano pool)
+    nano_cpu_workers_per_gpu_target: int = -1
     # run the per-GPU kernel broker in the executor daemon
     broker_enabled: bool = True
     # zygote processes forking light sandboxes per GPU (fork parallelism)

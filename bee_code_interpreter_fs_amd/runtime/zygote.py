@@ -37,6 +37,28 @@ _SPAWN_ENV_KEYS = ("BEE_WORKER_ID", "BEE_SANDBOX_DIR", "BEE_WORKSPACE", "BEE_RUN
 PR_SET_DUMPABLE = 4
 
 
+def _site_dirs_without_hooks() -> None:
+    """A zygote started with ``python -S`` (kind nano, csrc/executor/sandbox.cpp
+    start_zygote): site-packages go on sys.path where ``site`` would put them,
+    but no .pth file or sitecustomize runs.  On this image those start-up
+    hooks import ~30 modules (certifi -> importlib.resources -> pathlib,
+    tempfile, zipfile, shutil, bz2, lzma, ...) that every sandbox forked from
+    the zygote would copy at the fork and tear down at the exit: 109 -> 87
+    mappings, 8.0 -> 6.5 MB private memory.  User code keeps the same import
+    path; only .pth-installed path hooks are absent."""
+    if not sys.flags.no_site:
+        return
+    import site
+
+    dirs = []
+    if site.check_enableusersite():
+        dirs.append(site.getusersitepackages())
+    dirs += site.getsitepackages()
+    for d in dirs:
+        if os.path.isdir(d) and d not in sys.path:
+            sys.path.append(d)
+
+
 def _preload() -> list:
     os.environ.setdefault("MPLBACKEND", "Agg")
     names = [n.strip() for n in os.environ.get("BEE_PRELOAD", DEFAULT_PRELOAD).split(",") if n.strip()]
@@ -180,6 +202,7 @@ def main() -> None:
     # collapsed once the preload is done)
     thp = _thp_module()
     thp_on = bool(thp is not None and thp.thp_arenas())
+    _site_dirs_without_hooks()
     loaded = _preload()
     import_ms = (time.perf_counter() - t0) * 1e3
     if _hip_initialized():

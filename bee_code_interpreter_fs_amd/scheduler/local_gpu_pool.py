@@ -233,6 +233,7 @@ class LocalGpuPoolBackend(CodeExecutor):
                         "--min-cpu-target", str(c.min_cpu_workers_per_gpu_target),
                         "--nano-target", str(c.nano_workers_per_gpu_target),
                         "--nano-zygotes", str(c.nano_zygotes_per_gpu),
+                        "--nano-cpu-target", str(c.nano_cpu_workers_per_gpu_target),
                         "--gang-grace", str(c.gang_failure_grace_s),
                         # admission for every front-end replica of the node
                         "--max-inflight", str(max(c.max_inflight_per_gpu, 0)),
@@ -263,7 +264,8 @@ class LocalGpuPoolBackend(CodeExecutor):
                     and st.get("ready_light", 0) >= st.get("light_target", 0)
                     and st.get("ready_min", 0) >= st.get("min_target", 0)
                     and st.get("ready_min_cpu", 0) >= st.get("min_cpu_target", 0)
-                    and st.get("ready_nano", 0) >= st.get("nano_target", 0))
+                    and st.get("ready_nano", 0) >= st.get("nano_target", 0)
+                    and st.get("ready_nano_cpu", 0) >= st.get("nano_cpu_target", 0))
 
         while loop.time() < deadline:
             try:
@@ -565,10 +567,11 @@ def _mode_of_source(source: str) -> str:
     mods = imported_modules(source)
     if DIRECT_GPU_MODULES.intersection(mods):
         return "direct"
-    if all(m in GPU_API_MODULES or m in _STDLIB for m in mods) and GPU_API_MODULES.intersection(mods):
+    if all(m in GPU_API_MODULES or m in _STDLIB for m in mods):
         # beekern + stdlib: a sandbox from a zygote that never imported numpy
-        # (executor kind nano; the daemon falls back to a minimal one)
-        return "nano"
+        # (executor kind nano; the daemon falls back to a minimal one);
+        # stdlib only: the same, with its broker session opened on first use
+        return "nano" if GPU_API_MODULES.intersection(mods) else "nano_cpu"
     if all(m in MIN_MODULES or m in _STDLIB for m in mods):
         # numpy/beekern/stdlib only: the fast-forking minimal zygote; scripts
         # that never import beekern take a sandbox whose broker session opens

@@ -101,6 +101,10 @@ WORKLOADS = {
 }
 
 
+# the sandbox kind each workload's payload is routed to
+ROUTED_POOL = {"numpy_gpu": "nano", "numpy_cpu": "min", "fib": "nano_cpu", "hello": "nano_cpu", "scientific": "light"}
+
+
 def parse_args():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -245,6 +249,11 @@ def start_service(tmp: str, n_gpus: int, args):
     # GPU) what it is on one GPU -- weak scaling of the front-end too (24 at
     # N = 8; front-ends hold no GPU context)
     frontends = args.frontends or min(32, 3 * max(1, n_gpus))
+    routed = None if args.payload else ROUTED_POOL[args.workload]
+
+    def pool(kind: str) -> str:
+        return str(args.pool_target if routed is None or routed == kind else min(args.pool_target, 4))
+
     env = dict(os.environ)
     env.update(
         {
@@ -256,10 +265,12 @@ def start_service(tmp: str, n_gpus: int, args):
             "APP_FILE_STORAGE_PATH": os.path.join(tmp, "files"),
             "APP_SANDBOX_ROOT": os.path.join(tmp, "sandboxes"),
             "APP_WORKERS_PER_GPU_TARGET": "1",  # direct sandboxes: the payload does not need them
-            # the payloads import only beekern/numpy/stdlib -> minimal sandboxes
-            "APP_MIN_WORKERS_PER_GPU_TARGET": str(args.pool_target),
-            # beekern + stdlib payloads (the headline): numpy-free zygotes
-            "APP_NANO_WORKERS_PER_GPU_TARGET": os.environ.get("APP_NANO_WORKERS_PER_GPU_TARGET", str(args.pool_target)),
+            # the pool the workload's payload routes to (local_gpu_pool.py
+            # _mode_of_source) gets --pool-target warm sandboxes per GPU, the
+            # others a few: fewer idle processes on an 8-GPU node
+            "APP_MIN_WORKERS_PER_GPU_TARGET": pool("min"),
+            "APP_NANO_WORKERS_PER_GPU_TARGET": os.environ.get("APP_NANO_WORKERS_PER_GPU_TARGET", pool("nano")),
+            "APP_NANO_CPU_WORKERS_PER_GPU_TARGET": pool("nano_cpu"),
             # light sandboxes (pandas/scipy/matplotlib preloaded) serve the
             # scientific workload; the others only keep a few warm
             "APP_LIGHT_WORKERS_PER_GPU_TARGET": str(args.pool_target if args.workload == "scientific" else 4),

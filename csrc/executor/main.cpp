@@ -136,6 +136,7 @@ int main(int argc, char** argv) {
     else if (a == "--min-preload") cfg.min_preload = val();
     else if (a == "--nano-target") cfg.nano_target = atoi(val().c_str());
     else if (a == "--nano-zygotes") cfg.nano_zygotes = atoi(val().c_str());
+    else if (a == "--nano-cpu-target") cfg.nano_cpu_target = atoi(val().c_str());
     else if (a == "--nano-preload") cfg.nano_preload = val();
     else if (a == "--runtime-packages") cfg.pod_runtime_packages = val();
     else if (a == "--cpus") cpus_spec = val();

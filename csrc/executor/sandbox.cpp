@@ -85,6 +85,7 @@ const char* kind_name(int kind) {
     case kMin: return "min";
     case kMinCpu: return "min_cpu";
     case kNano: return "nano";
+    case kNanoCpu: return "nano_cpu";
   }
   return "?";
 }
@@ -405,7 +406,12 @@ bool SandboxPool::start_zygote(Zygote* z, std::string* err) {
   std::vector<char*> envp;
   for (auto& s : env_store) envp.push_back(const_cast<char*>(s.c_str()));
   envp.push_back(nullptr);
+  // nano zygotes skip `site` (-S): the zygote puts site-packages on sys.path
+  // itself, without the .pth / sitecustomize start-up hooks whose imports
+  // every forked sandbox would otherwise carry (runtime/zygote.py)
   std::vector<std::string> args = {cfg_.python, "-u", "-m", cfg_.zygote_module};
+  const char* no_site = getenv("BEE_NANO_NO_SITE");  // "0": keep `site` (A/B)
+  if (z->kind == kNano && !(no_site && strcmp(no_site, "0") == 0)) args.insert(args.begin() + 2, "-S");
   std::vector<char*> argv;
   for (auto& a : args) argv.push_back(const_cast<char*>(a.c_str()));
   argv.push_back(nullptr);
@@ -457,7 +463,8 @@ Zygote* SandboxPool::pick_zygote(int kind) {
   std::vector<Zygote*> same, light;
   for (auto& z : zygotes_) {
     if (!z->alive) continue;
-    if (z->kind == kind || (kind == kMinCpu && z->kind == kMin)) same.push_back(z.get());
+    if (z->kind == kind || (kind == kMinCpu && z->kind == kMin) || (kind == kNanoCpu && z->kind == kNano))
+      same.push_back(z.get());
     if (z->kind == kLight) light.push_back(z.get());
   }
   if (!same.empty()) return same[rr_++ % same.size()];
@@ -772,7 +779,7 @@ std::shared_ptr<Worker> SandboxPool::spawn_worker(bool pooled, int kind, const s
   const bool warm = pooled && kind == kDirect && cfg_.warm_gpu && !gpus.empty();
   if (warm) env.set("BEE_WARM_GPU", "1");
   if (kind != kDirect && broker_) env.set("BEE_BROKER_SOCK", broker_->socket_path());
-  if (kind == kMinCpu) env.set("BEE_BROKER_LAZY", "1");
+  if (kind == kMinCpu || kind == kNanoCpu) env.set("BEE_BROKER_LAZY", "1");
   if (cfg_.default_hbm_quota > 0) env.set("BEE_HBM_QUOTA_BYTES", std::to_string(cfg_.default_hbm_quota));
   for (auto& kv : extra_env.as_object()) env.set(kv.first, kv.second.is_string() ? kv.second : Json(kv.second.dump()));
 
@@ -827,6 +834,8 @@ int SandboxPool::target_of(int kind) const {
   if (kind == kMin) return light_ok_ && min_ok_ ? cfg_.min_target : 0;
   if (kind == kMinCpu) return broker_ && min_ok_ ? (cfg_.min_cpu_target >= 0 ? cfg_.min_cpu_target : cfg_.min_target) : 0;
   if (kind == kNano) return light_ok_ && nano_ok_ ? cfg_.nano_target : 0;
+  if (kind == kNanoCpu)
+    return broker_ && nano_ok_ ? (cfg_.nano_cpu_target >= 0 ? cfg_.nano_cpu_target : cfg_.nano_target) : 0;
   return cfg_.target;
 }
 
@@ -1468,6 +1477,10 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
                    : mode == "min_cpu" ? (target_of(kMinCpu) > 0 ? kMinCpu : min_ok_ ? kMin : kLight)
                    : mode == "min" ? (min_ok_ ? kMin : kLight)
                    : mode == "nano" ? (nano_ok_ ? kNano : min_ok_ ? kMin : kLight)
+                   : mode == "nano_cpu" ? (target_of(kNanoCpu) > 0 ? kNanoCpu
+                                           : nano_ok_ ? kNano
+                                           : target_of(kMinCpu) > 0 ? kMinCpu
+                                           : min_ok_ ? kMin : kLight)
                    : mode == "light" ? kLight
                                      : kDirect;
   if (!dedicated) {
@@ -1815,6 +1828,7 @@ Json SandboxPool::status() {
   j.set("min_target", target_of(kMin));
   j.set("min_cpu_target", target_of(kMinCpu));
   j.set("nano_target", target_of(kNano));
+  j.set("nano_cpu_target", target_of(kNanoCpu));
   {
     // per executed sandbox: its whole CPU (the zygote's wait4, teardown
     // included) against what it reported itself before exiting
@@ -1838,6 +1852,7 @@ Json SandboxPool::status() {
   for (int k = 0; k < kNumKinds; ++k) ready_all += (int64_t)ready_[k].size(), spawning_all += spawning_[k];
   j.set("ready", ready_all);
   j.set("ready_nano", (int64_t)ready_[kNano].size());
+  j.set("ready_nano_cpu", (int64_t)ready_[kNanoCpu].size());
   j.set("ready_min_cpu", (int64_t)ready_[kMinCpu].size());
   j.set("ready_min", (int64_t)ready_[kMin].size());
   j.set("ready_direct", (int64_t)ready_[kDirect].size());
@@ -1955,6 +1970,7 @@ std::string SandboxPool::metrics_text() {
   for (int k = 0; k < kNumKinds; ++k) ready_all += (double)ready_[k].size(), spawning_all += spawning_[k];
   line("bee_executor_ready_workers", "gauge", ready_all);
   line("bee_executor_ready_nano_workers", "gauge", (double)ready_[kNano].size());
+  line("bee_executor_ready_nano_cpu_workers", "gauge", (double)ready_[kNanoCpu].size());
   line("bee_executor_ready_min_workers", "gauge", (double)ready_[kMin].size());
   line("bee_executor_ready_light_workers", "gauge", (double)ready_[kLight].size());
   line("bee_executor_ready_min_cpu_workers", "gauge", (double)ready_[kMinCpu].size());

@@ -46,7 +46,7 @@ class ServiceHarness:
             executor_backend="local",
             # a small numpy-free pool: enough to serve the tests that route
             # there, without 16 more sandboxes per service on the CPU runner
-            nano_workers_per_gpu_target=2,
+            nano_workers_per_gpu_target=6,
             nano_zygotes_per_gpu=1,
         )
         base.update(overrides)

@@ -369,7 +369,7 @@ def test_sandbox_mode_routing(tmp_path):
 
     st = Storage(str(tmp_path))
     mode = lambda src: sandbox_mode(ExecuteRequest(source_code=src), st)  # noqa: E731
-    assert mode("print(1)") == "min_cpu"  # no GPU module: lazy broker session
+    assert mode("print(1)") == "nano_cpu"  # stdlib only: numpy-free zygote, lazy broker session
     assert mode("import numpy as np, time, json") == "min_cpu"
     assert mode("import numpy as np, time, json\nimport beekern as bk") == "min"
     assert mode("from bee_code_interpreter_fs_amd import ops") == "nano"
