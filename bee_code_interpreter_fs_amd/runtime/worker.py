@@ -252,7 +252,44 @@ def warm_gpu() -> Optional[str]:
         return f"{type(e).__name__}: {e}"
 
 
-def _run_main(path: str, lowered: Optional[str] = None) -> None:
+_MAGIC: list = []  # the interpreter's bytecode magic, resolved once
+
+
+def load_precompiled(blob: str, path: str):
+    """(code object, needs the shell runtime) from the front-end's
+    precompiled payload (scheduler/local_gpu_pool.py precompiled), with every
+    code object's file name set to ``path`` as compile(source, path) would
+    have; None when the blob is not for this interpreter or does not decode
+    (the worker then compiles the source itself)."""
+    import binascii
+    import marshal
+
+    if not _MAGIC:
+        import importlib.util
+
+        _MAGIC.append(importlib.util.MAGIC_NUMBER)
+    try:
+        raw = binascii.a2b_base64(blob)
+    except (binascii.Error, ValueError):
+        return None
+    magic = _MAGIC[0]
+    if raw[: len(magic)] != magic or raw[len(magic): len(magic) + 1] not in (b"P", b"X"):
+        return None
+    try:
+        code = marshal.loads(raw[len(magic) + 1:])
+    except (EOFError, ValueError, TypeError):
+        return None
+    if not isinstance(code, types.CodeType):
+        return None
+
+    def rename(c):
+        consts = tuple(rename(k) if isinstance(k, types.CodeType) else k for k in c.co_consts)
+        return c.replace(co_filename=path, co_consts=consts)
+
+    return rename(code), raw[len(magic): len(magic) + 1] == b"X"
+
+
+def _run_main(path: str, lowered: Optional[str] = None, code=None, shell: bool = False) -> None:
     """`python path` semantics (what runpy.run_path does for a plain file,
     minus its zip/directory probing): compile, bind a fresh ``__main__``
     module, execute.  ``lowered``: the payload with its xonsh shell lines
@@ -260,16 +297,18 @@ def _run_main(path: str, lowered: Optional[str] = None) -> None:
     tracebacks point at the user's lines.  The module is left alive -- the
     process ends with os._exit, and the broker releases device memory on
     disconnect -- so no teardown work lands on the request path."""
-    if lowered is None:
-        with io.open_code(path) as fh:
-            source = fh.read()
-    else:
-        source = lowered
-    code = compile(source, path, "exec", dont_inherit=True)
+    if code is None:
+        if lowered is None:
+            with io.open_code(path) as fh:
+                source = fh.read()
+        else:
+            source = lowered
+        code = compile(source, path, "exec", dont_inherit=True)
+        shell = lowered is not None
     mod = types.ModuleType("__main__")
     mod.__dict__.update({"__file__": path, "__cached__": None, "__loader__": None, "__package__": None,
                          "__spec__": None, "__builtins__": builtins})
-    if lowered is not None:
+    if shell:
         from . import xsh
 
         mod.__dict__[xsh.RUNTIME_NAME] = xsh.Runtime()
@@ -301,7 +340,7 @@ def _prepare_paths(runtime_packages: str) -> None:
     _PATHS_FOR[:] = [runtime_packages]
 
 
-def run_script(script: str, argv, workspace: str, runtime_packages: str) -> int:
+def run_script(script: str, argv, workspace: str, runtime_packages: str, precompiled: Optional[str] = None) -> int:
     sys.argv = [script, *argv]
     script_dir = os.path.dirname(os.path.abspath(script))
     if _PATHS_FOR != [runtime_packages]:
@@ -311,6 +350,7 @@ def run_script(script: str, argv, workspace: str, runtime_packages: str) -> int:
 
     sandbox_patches.install()
     lowered = None
+    pre = load_precompiled(precompiled, script) if precompiled else None
     try:
         with open(script, "rb") as fh:
             source = fh.read().decode("utf-8", errors="replace")
@@ -318,15 +358,20 @@ def run_script(script: str, argv, workspace: str, runtime_packages: str) -> int:
         from .deps import install_missing
 
         # xonsh-style shell lines (the reference ran every payload through
-        # xonsh): lowered to Python here, plain Python passes untouched
-        lowered = xsh.lower_payload(source)
+        # xonsh): lowered to Python here, plain Python passes untouched --
+        # unless the front-end already compiled the payload (lowering included)
+        if pre is None:
+            lowered = xsh.lower_payload(source)
         install_missing(lowered or source, runtime_packages)
     except OSError:
         pass
     code = 0
     _STAMPS["script_start"] = time.monotonic() * 1e3
     try:
-        _run_main(script, lowered)
+        if pre is not None:
+            _run_main(script, code=pre[0], shell=pre[1])
+        else:
+            _run_main(script, lowered)
     except SystemExit as e:
         if e.code is None:
             code = 0
@@ -661,5 +706,5 @@ def _serve(cwd: str, chan: _Chan) -> None:
         script = _to_logical(script, cwd, ws_view)
         if rp and rp_view:
             script = _to_logical(script, rp, rp_view)
-    code = run_script(script, job.get("argv") or [], ws_view, rp_view)
+    code = run_script(script, job.get("argv") or [], ws_view, rp_view, job.get("code"))
     _finish(code, os.path.join(os.path.dirname(job["stdout"]), "timing.json"), chan)

@@ -259,6 +259,7 @@ class SandboxPool {
     double timeout_s = 60;
     int64_t hbm_quota = 0;
     Json env = Json::object();
+    std::string code;  // the front-end's precompiled payload (opaque to the daemon), "" = none
   };
   struct RunResult {
     std::string stdout_text, stderr_text;

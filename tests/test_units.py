@@ -535,3 +535,32 @@ def test_beekern_imports_without_numpy_and_fill_patterns_match():
     assert got == [int(x) for x in ref]
     assert _lazy.scalar(1.5) == 1.5 and isinstance(_lazy.scalar(1.5), np.float64)  # numpy loaded here
     assert _lazy.is_number(np.float32(2)) and _lazy.is_integer(np.int64(3)) and not _lazy.is_integer(2.0)
+
+
+def test_precompiled_payload_roundtrip():
+    """The front-end's precompiled payload (local_gpu_pool.precompiled) loads
+    in the worker as the code compile(source, path) gives -- every nested code
+    object renamed to the sandbox's script path -- and anything odd falls
+    back to the worker's own compile (None)."""
+    import types
+
+    from bee_code_interpreter_fs_amd.runtime.worker import load_precompiled
+    from bee_code_interpreter_fs_amd.scheduler.local_gpu_pool import precompiled
+
+    src = "def f(x):\n    return [i * x for i in range(3)]\nprint(f(2))\n"
+    blob = precompiled(src)
+    code, shell = load_precompiled(blob, "/workspace/main.py")
+    ref = compile(src, "/workspace/main.py", "exec", dont_inherit=True)
+    assert not shell and code.co_code == ref.co_code
+
+    def names(c):
+        yield c.co_filename
+        for k in c.co_consts:
+            if isinstance(k, types.CodeType):
+                yield from names(k)
+
+    assert set(names(code)) == {"/workspace/main.py"}
+    assert precompiled("print(\n") is None  # the sandbox reports the SyntaxError itself
+    assert load_precompiled(precompiled("echo hi\n"), "/x.py")[1] is True  # xonsh-lowered
+    assert load_precompiled("not base64 !", "/x.py") is None
+    assert load_precompiled(__import__("base64").b64encode(b"\0\0\0\0P...").decode(), "/x.py") is None
