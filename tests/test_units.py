@@ -564,3 +564,11 @@ def test_precompiled_payload_roundtrip():
     assert load_precompiled(precompiled("echo hi\n"), "/x.py")[1] is True  # xonsh-lowered
     assert load_precompiled("not base64 !", "/x.py") is None
     assert load_precompiled(__import__("base64").b64encode(b"\0\0\0\0P...").decode(), "/x.py") is None
+
+
+def test_precompile_only_repeated_sources():
+    from bee_code_interpreter_fs_amd.scheduler import local_gpu_pool as lgp
+
+    src = "print('precompile-once-%d')\n" % os.getpid()
+    assert lgp.precompiled_if_repeated(src) is None  # first sight: the sandbox compiles
+    assert lgp.precompiled_if_repeated(src) == lgp.precompiled(src)  # seen before: shipped compiled
