@@ -20,10 +20,12 @@ asks for (~80 ms saved) and what the examples need.
 
 from __future__ import annotations
 
+import binascii  # precompiled payloads (load_precompiled): imported pre-fork
 import builtins
 import ctypes
 import io
 import json
+import marshal
 import os
 import resource
 import socket
@@ -252,7 +254,7 @@ def warm_gpu() -> Optional[str]:
         return f"{type(e).__name__}: {e}"
 
 
-_MAGIC: list = []  # the interpreter's bytecode magic, resolved once
+from importlib.util import MAGIC_NUMBER as _MAGIC  # noqa: E402 - the interpreter's bytecode magic, pre-fork
 
 
 def load_precompiled(blob: str, path: str):
@@ -261,18 +263,11 @@ def load_precompiled(blob: str, path: str):
     code object's file name set to ``path`` as compile(source, path) would
     have; None when the blob is not for this interpreter or does not decode
     (the worker then compiles the source itself)."""
-    import binascii
-    import marshal
-
-    if not _MAGIC:
-        import importlib.util
-
-        _MAGIC.append(importlib.util.MAGIC_NUMBER)
     try:
         raw = binascii.a2b_base64(blob)
     except (binascii.Error, ValueError):
         return None
-    magic = _MAGIC[0]
+    magic = _MAGIC
     if raw[: len(magic)] != magic or raw[len(magic): len(magic) + 1] not in (b"P", b"X"):
         return None
     try:
