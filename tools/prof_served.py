@@ -36,7 +36,8 @@ def cmd(d: str) -> None:
     from bee_code_interpreter_fs_amd.scheduler.executor_process import ExecutorProcess
 
     ex = ExecutorProcess("prof", os.path.join(d, "sandboxes"), gpus="0", target=1, light_target=2, broker=True,
-                         light_zygotes=1, extra_args=["--min-target", "8", "--min-zygotes", "2"])
+                         light_zygotes=1, extra_args=["--min-target", "2", "--min-zygotes", "1",
+                                                    "--nano-target", "8", "--nano-zygotes", "2"])
     for a in ex.command(sock_path(d)):
         print(a)
 
@@ -53,7 +54,7 @@ async def _drive(d: str, n: int, conc: int) -> dict:
     client = UdsHttpClient(path)
     for _ in range(150):  # warm pool (30 s at most)
         st = (await client.request("GET", "/v1/status", None, 10)).json()
-        if st.get("ready_min", 0) >= 1:
+        if st.get("ready_nano", 0) >= 1:
             break
         await asyncio.sleep(0.2)
     src = open(PAYLOAD).read()
@@ -67,7 +68,7 @@ async def _drive(d: str, n: int, conc: int) -> dict:
         while left[0] > 0:
             left[0] -= 1
             t = time.perf_counter()
-            body = {"source_code": src, "timeout": 120, "collect_dir": collect, "mode": "min", "files": {}}
+            body = {"source_code": src, "timeout": 120, "collect_dir": collect, "mode": "nano", "files": {}}
             r = await client.request("POST", "/v1/execute", json.dumps(body).encode(), 300)
             lat.append((time.perf_counter() - t) * 1e3)
             if r.status_code != 200 or r.json().get("exit_code") != 0:
