@@ -283,7 +283,42 @@ __global__ __launch_bounds__(256) void gemm_bf16_tn_skinny(const uint16_t* __res
   for (int i = 0; i < kSkinnyRows; ++i)
 #pragma unroll
     for (int j = 0; j < kSkinnyCols; ++j) acc[i][j] = 0.f;
-  for (int k = lane * 8; k < K; k += 512) {  // K % 8 == 0: chunks are whole
+  // four K steps' loads in flight per lane (the GEMV shape is latency-bound:
+  // 4096^2 . 4096 ran 9.4 us with one step at a time); the FMAs still run
+  // step by step, so the sums are the one-step loop's
+  constexpr int KB = 4;
+  int k = lane * 8;
+  for (; k + (KB - 1) * 512 < K; k += KB * 512) {
+    uint4 qa[KB][kSkinnyRows];
+#pragma unroll
+    for (int s = 0; s < KB; ++s)
+#pragma unroll
+      for (int i = 0; i < kSkinnyRows; ++i) {
+        const int64_t row = min(row0 + i, (int64_t)M - 1);
+        qa[s][i] = *reinterpret_cast<const uint4*>(A + row * lda + k + s * 512);
+      }
+#pragma unroll
+    for (int j = 0; j < kSkinnyCols; ++j) {
+      if (j >= r) break;
+      uint4 qb[KB];
+#pragma unroll
+      for (int s = 0; s < KB; ++s) qb[s] = *reinterpret_cast<const uint4*>(Bt + (int64_t)j * ldb + k + s * 512);
+#pragma unroll
+      for (int s = 0; s < KB; ++s) {
+        const uint32_t wb[4] = {qb[s].x, qb[s].y, qb[s].z, qb[s].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float b0 = bf16_bits_to_float((uint16_t)(wb[e] & 0xffff)), b1 = bf16_bits_to_float((uint16_t)(wb[e] >> 16));
+#pragma unroll
+          for (int i = 0; i < kSkinnyRows; ++i) {
+            const uint32_t wa = e == 0 ? qa[s][i].x : e == 1 ? qa[s][i].y : e == 2 ? qa[s][i].z : qa[s][i].w;
+            acc[i][j] += bf16_bits_to_float((uint16_t)(wa & 0xffff)) * b0 + bf16_bits_to_float((uint16_t)(wa >> 16)) * b1;
+          }
+        }
+      }
+    }
+  }
+  for (; k < K; k += 512) {  // K % 8 == 0: chunks are whole
     float a[kSkinnyRows][8];
 #pragma unroll
     for (int i = 0; i < kSkinnyRows; ++i) {
