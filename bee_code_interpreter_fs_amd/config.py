@@ -180,6 +180,13 @@ class Config:
     # a gang whose rank failed: seconds the other ranks get to finish before
     # the whole gang is killed (they are usually stuck in a collective)
     gang_failure_grace_s: float = 10.0
+    # environment for every rank of a multi-GPU gang, set by the executor
+    # under the request's own NCCL_* entries (operators may set HSA_* here,
+    # requests may not).  A gang is one node's GPUs over xGMI: InfiniBand /
+    # RoCE probing at communicator init is skipped.  Channel / protocol knobs
+    # (NCCL_MIN_NCHANNELS, NCCL_PROTO, ...) are left to RCCL's gfx950 tuning
+    # tables unless set here for a measured reason
+    gang_rccl_env: Dict[str, str] = field(default_factory=lambda: {"NCCL_IB_DISABLE": "1"})
     # processes + threads per sandbox tree (the executor's monitor, any
     # mode; plus RLIMIT_NPROC of the sandbox UID in UID mode)
     sandbox_max_processes: int = 1024

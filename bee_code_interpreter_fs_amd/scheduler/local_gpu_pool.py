@@ -236,6 +236,8 @@ class LocalGpuPoolBackend(CodeExecutor):
                         "--nano-zygotes", str(c.nano_zygotes_per_gpu),
                         "--nano-cpu-target", str(c.nano_cpu_workers_per_gpu_target),
                         "--gang-grace", str(c.gang_failure_grace_s),
+                        "--gang-env", ",".join(f"{k}={v}" for k, v in sorted((c.gang_rccl_env or {}).items())
+                                               if "," not in f"{k}={v}"),
                         # admission for every front-end replica of the node
                         "--max-inflight", str(max(c.max_inflight_per_gpu, 0)),
                         "--hbm-capacity", str(self.hbm_capacity if gpu is not None else 0),

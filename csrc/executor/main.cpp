@@ -147,6 +147,18 @@ int main(int argc, char** argv) {
     else if (a == "--nproc") cfg.nproc = atoll(val().c_str());
     else if (a == "--mem-limit") cfg.mem_bytes = atoll(val().c_str());
     else if (a == "--gang-grace") cfg.gang_grace_s = atof(val().c_str());
+    else if (a == "--gang-env") {
+      const std::string spec = val();
+      size_t i = 0;
+      while (i < spec.size()) {
+        size_t j = spec.find(',', i);
+        if (j == std::string::npos) j = spec.size();
+        const std::string kv = spec.substr(i, j - i);
+        const size_t eq = kv.find('=');
+        if (eq != std::string::npos && eq > 0) cfg.gang_env.emplace_back(kv.substr(0, eq), kv.substr(eq + 1));
+        i = j + 1;
+      }
+    }
     else if (a == "--hbm-watchdog-ms") cfg.hbm_watchdog_ms = atoi(val().c_str());
     else if (a == "--hbm-slack") cfg.hbm_slack = atoll(val().c_str());
     else if (a == "--max-inflight") cfg.max_inflight = atoi(val().c_str());

@@ -1515,6 +1515,10 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
         e2.set("BEE_GANG_RDZV", rdzv);
         // RCCL's bootstrap sockets: loopback only (a gang never leaves the node)
         if (!e2.has("NCCL_SOCKET_IFNAME")) e2.set("NCCL_SOCKET_IFNAME", "lo");
+        // the operator's RCCL policy for single-node gangs (config
+        // gang_rccl_env), under the request's own NCCL_* choices
+        for (auto& kv : cfg_.gang_env)
+          if (!e2.has(kv.first)) e2.set(kv.first, kv.second);
       }
       std::lock_guard<std::mutex> lk(mu_);
       // ranks > 0 also see rank 0's tmp, where a source_code script lands

@@ -378,22 +378,24 @@ __global__ __launch_bounds__(256) void rowsum_v(const T* __restrict__ x, int64_t
   const int lane = threadIdx.x & 63;
   const V16<T>* p = reinterpret_cast<const V16<T>*>(x + row * ld);
   const int64_t nv = cols / V;
-  double a0 = 0.0, a1 = 0.0;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   int64_t c = lane;
-  for (; c + 64 < nv; c += 128) {  // two vectors in flight per lane
-    const V16<T> u = p[c], w = p[c + 64];
+  for (; c + 192 < nv; c += 256) {  // four vectors in flight per lane
+    const V16<T> u = p[c], w = p[c + 64], y = p[c + 128], z = p[c + 192];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       a0 += to_f64<T>(u.v[j]);
       a1 += to_f64<T>(w.v[j]);
+      a2 += to_f64<T>(y.v[j]);
+      a3 += to_f64<T>(z.v[j]);
     }
   }
-  if (c < nv) {
+  for (; c < nv; c += 64) {
     const V16<T> u = p[c];
 #pragma unroll
     for (int j = 0; j < V; ++j) a0 += to_f64<T>(u.v[j]);
   }
-  const double acc = wave_reduce<kRedSum>(a0 + a1);
+  const double acc = wave_reduce<kRedSum>((a0 + a1) + (a2 + a3));
   if (lane == 0) out[row] = (TO)(acc * scale);
 }
 

@@ -105,3 +105,31 @@ def test_idle_sandboxes_are_recycled(tmp_path):
     recycled = [l for l in metrics.splitlines() if l.startswith("bee_executor_idle_recycled_total")]
     assert recycled and float(recycled[0].split()[-1]) >= 1, metrics
     assert body["stdout"] == "5\n"
+
+
+def test_gang_ranks_get_the_operator_rccl_env(tmp_path):
+    """--gang-env (config gang_rccl_env): every gang rank gets the operator's
+    RCCL policy, a request's own NCCL_* entry wins over it, and a non-gang
+    sandbox gets none of it."""
+    ensure_native_executor()
+    code = "import os\nprint(os.environ.get('RANK'), os.environ.get('NCCL_IB_DISABLE'), os.environ.get('NCCL_PROTO'))\n"
+
+    async def go():
+        ex = ExecutorProcess("gang", str(tmp_path / "sb"), gpus="", target=1,
+                             extra_args=["--gang-env", "NCCL_IB_DISABLE=1,NCCL_PROTO=Simple"])
+        await ex.start()
+        try:
+            await ex.wait_ready(1, 120)
+            gang = await ex.post("/v1/execute", {"source_code": code, "nprocs": 2, "gpus": "", "timeout": 60,
+                                                 "env": {"NCCL_PROTO": "LL128"}, "collect_dir": str(tmp_path)},
+                                 timeout=120)
+            one = await ex.post("/v1/execute", {"source_code": code, "timeout": 60, "collect_dir": str(tmp_path)},
+                                timeout=120)
+            return gang.json(), one.json()
+        finally:
+            await ex.close()
+
+    gang, one = asyncio.run(go())
+    assert gang["exit_code"] == 0, gang["stderr"]
+    assert sorted(gang["stdout"].splitlines()) == ["0 1 LL128", "1 1 LL128"], gang["stdout"]
+    assert one["stdout"] == "None None None\n", one
