@@ -299,57 +299,73 @@ __global__ __launch_bounds__(256) void colsum_1pass(const T* __restrict__ x, int
   if (threadIdx.x == 0) rearm(tickets + blockIdx.x);
 }
 
-// 16-B vectors per lane (V columns), G row groups (waves) per block: a wave
-// reads one contiguous 1 KiB row segment per step, and every lane has its
-// rows' loads in flight four at a time.  G = 16 (1024 threads): the 4096^2
-// bf16 column sum of the headline payload keeps 4x the bytes in flight of
-// the 4-wave version (512 blocks on 256 CUs), 15.4 us -> see profiles.
-template <typename T, typename TO, int G>
-__global__ __launch_bounds__(G * 64) void colsum_1pass_v(const T* __restrict__ x, int64_t rows, int64_t cols,
-                                                         int64_t ld, int64_t rows_per_chunk, double* __restrict__ part,
-                                                         unsigned* __restrict__ tickets, TO* __restrict__ out,
-                                                         double scale) {
+// Column sums, 16-B vectors: a block of 16 waves owns a 16*V-column strip
+// (bf16: 128 columns) of one row chunk.  A wave covers 4 rows x the strip
+// per step (16 lanes per row: 256-B row segments), the block 64 rows, and
+// every lane has up to four steps' loads in flight.  Lanes 16 apart hold the
+// same columns: the wave folds them with cross-lane moves (fixed order), the
+// block folds its 16 waves through 16 KiB of LDS, and one f64 partial per
+// column and chunk goes to the workspace.  The last block of each strip
+// (completion ticket) folds the strip's chunk partials in chunk order.  Narrow
+// strips keep the chunk count low (4096^2: 32 strips x 32 chunks) -- the
+// 512-column version spent most of its 13.6-15.4 us folding 64 chunks.
+constexpr int kColWaves = 16;
+
+template <typename T, typename TO>
+__global__ __launch_bounds__(kColWaves * 64) void colsum_tile_v(const T* __restrict__ x, int64_t rows, int64_t cols,
+                                                              int64_t ld, int64_t rows_per_chunk,
+                                                              double* __restrict__ part, unsigned* __restrict__ tickets,
+                                                              TO* __restrict__ out, double scale) {
   constexpr int V = 16 / sizeof(T);
-  constexpr int NT = G * 64;
-  __shared__ double sacc[G][64 * V];
-  const int tx = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int64_t col0 = ((int64_t)blockIdx.x * 64 + tx) * V;
+  constexpr int W = 16 * V;  // strip width (columns)
+  __shared__ double sacc[kColWaves][W];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cl = lane & 15, rl = lane >> 4;  // column lane, row lane
+  const int64_t col0 = (int64_t)blockIdx.x * W + cl * V;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
   const int64_t r1 = r0 + rows_per_chunk < rows ? r0 + rows_per_chunk : rows;
+  constexpr int kStep = kColWaves * 4;  // rows per block step
   double acc[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) acc[j] = 0.0;
   if (col0 < cols) {
-    int64_t r = r0 + g;
-    for (; r + 3 * G < r1; r += 4 * G) {  // four rows' loads issued before their adds (same order)
+    int64_t r = r0 + wave * 4 + rl;
+    for (; r + 3 * kStep < r1; r += 4 * kStep) {
       V16<T> v[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const V16<T>*>(x + (r + q * G) * ld + col0);
+      for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const V16<T>*>(x + (r + q * kStep) * ld + col0);
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int j = 0; j < V; ++j) acc[j] += to_f64<T>(v[q].v[j]);
     }
-    for (; r < r1; r += G) {
+    for (; r < r1; r += kStep) {
       const V16<T> v = *reinterpret_cast<const V16<T>*>(x + r * ld + col0);
 #pragma unroll
       for (int j = 0; j < V; ++j) acc[j] += to_f64<T>(v.v[j]);
     }
   }
+  // row lanes 0..3 of each column lane: (0 + 1) + (2 + 3), same in every lane
 #pragma unroll
-  for (int j = 0; j < V; ++j) sacc[g][tx * V + j] = acc[j];
+  for (int j = 0; j < V; ++j) {
+    acc[j] += __shfl_xor(acc[j], 16, 64);
+    acc[j] += __shfl_xor(acc[j], 32, 64);
+  }
+  if (rl == 0) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) sacc[wave][cl * V + j] = acc[j];
+  }
   __syncthreads();
-  // the block folds its G row groups of 64*V columns, group order fixed
-  for (int c = threadIdx.x; c < 64 * V; c += NT) {
-    const int64_t col = (int64_t)blockIdx.x * 64 * V + c;
+  if (threadIdx.x < W) {
+    const int64_t col = (int64_t)blockIdx.x * W + threadIdx.x;
     double s = 0.0;
 #pragma unroll
-    for (int q = 0; q < G; ++q) s += sacc[q][c];
+    for (int w = 0; w < kColWaves; ++w) s += sacc[w][threadIdx.x];
     if (col < cols) publish(part + (int64_t)blockIdx.y * cols + col, s);
   }
   if (!take_last_ticket(tickets + blockIdx.x, gridDim.y)) return;
-  for (int c = threadIdx.x; c < 64 * V; c += NT) {
-    const int64_t col = (int64_t)blockIdx.x * 64 * V + c;
+  if (threadIdx.x < W) {
+    const int64_t col = (int64_t)blockIdx.x * W + threadIdx.x;
     if (col < cols) out[col] = (TO)(fold_chunks(part, (int)gridDim.y, cols, col) * scale);
   }
   if (threadIdx.x == 0) rearm(tickets + blockIdx.x);
@@ -410,13 +426,18 @@ int launch_axis(const T* x, int64_t rows, int64_t cols, int64_t ld, int axis, TO
       rowsum<T, TO><<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(x, rows, cols, ld, out, scale);
     return launch_status();
   }
-  const bool vec = cols % V == 0 && ld % V == 0 && ((uintptr_t)x & 15) == 0;
-  const int64_t col_blocks = vec ? (cols + 64 * V - 1) / (64 * V) : (cols + 255) / 256;
+  // (strips of 16*V columns while the tickets go round; wider matrices take
+  // the scalar kernel's 256-column blocks)
+  const bool vec = cols % V == 0 && ld % V == 0 && ((uintptr_t)x & 15) == 0 &&
+                   (cols + 16 * V - 1) / (16 * V) <= kAxisTickets;
+  const int64_t col_blocks = vec ? (cols + 16 * V - 1) / (16 * V) : (cols + 255) / 256;
   // enough row chunks for ~1k blocks, as far as the workspace allows; each
-  // chunk at least 32 rows so a lane streams several vectors
+  // chunk at least 32 rows so a lane streams several vectors (vec: 128 rows,
+  // two 64-row steps of the 16-wave block)
   int64_t chunks = 1024 / col_blocks;
   if (chunks * cols > kAxisWsDoubles) chunks = kAxisWsDoubles / cols;
-  if (chunks > (rows + 31) / 32) chunks = (rows + 31) / 32;
+  const int64_t min_rows = vec ? 128 : 32;
+  if (chunks > (rows + min_rows - 1) / min_rows) chunks = (rows + min_rows - 1) / min_rows;
   if (chunks < 1) chunks = 1;
   const int64_t per = (rows + chunks - 1) / chunks;
   chunks = (rows + per - 1) / per;
@@ -424,7 +445,7 @@ int launch_axis(const T* x, int64_t rows, int64_t cols, int64_t ld, int axis, TO
   if (col_blocks > kAxisTickets) return kBadArgument;
   const dim3 grid((unsigned)col_blocks, (unsigned)chunks);
   if (vec)
-    colsum_1pass_v<T, TO, 16><<<grid, 16 * 64, 0, s>>>(x, rows, cols, ld, per, ws, tickets, out, scale);
+    colsum_tile_v<T, TO><<<grid, kColWaves * 64, 0, s>>>(x, rows, cols, ld, per, ws, tickets, out, scale);
   else
     colsum_1pass<T, TO><<<grid, 256, 0, s>>>(x, rows, cols, ld, per, ws, tickets, out, scale);
   return launch_status();

@@ -521,7 +521,7 @@ def test_bf16_uniform_is_rounded_f32_stream(gpu):
 
 
 @pytest.mark.parametrize("dtype", ["float64", "float32", "bfloat16"])
-@pytest.mark.parametrize("shape", [(1000, 300), (4096, 4096), (3, 70000), (70000, 3)])
+@pytest.mark.parametrize("shape", [(1000, 300), (4096, 4096), (3, 70000), (70000, 3), (2, 140000), (777, 4104)])
 def test_sum_mean_along_axis(gpu, dtype, shape):
     """bk.sum / bk.mean(axis=0|1) (bk_reduce_axis: column sums with chunked
     f64 partials + an ordered fold, row sums one wave per row) against fp64,
