@@ -33,6 +33,24 @@ def test_payload_runs_on_pinned_gpu(gsvc):
     assert r.gpu_ids == [0]
 
 
+def test_nano_sandbox_runs_beekern_without_numpy(gsvc):
+    """A beekern + stdlib script lands in a nano sandbox (zygote without
+    numpy, python -S): the broker path works, reductions come back as plain
+    floats, numpy is never imported -- and a script that asks for numpy
+    afterwards still gets numpy.float64 results."""
+    code = (
+        "import sys, beekern as bk\n"
+        "x = bk.random.rand(1 << 20)\n"
+        "s = bk.sum(bk.square(x))\n"
+        "print(round(s / (1 << 20), 2), type(s).__name__, 'numpy' in sys.modules, sys.flags.no_site, bk.driver_name())\n"
+        "np = __import__('num' + 'py')\n"
+        "print(type(bk.sum(x)).__name__)\n"
+    )
+    r = run(gsvc, code)
+    assert r.exit_code == 0, r.stderr
+    assert r.stdout.split() == ["0.33", "float", "False", "1", "broker", "float64"], r.stdout
+
+
 def test_sandbox_sees_only_its_gpu_and_is_warm(gsvc):
     code = (
         "import os, beekern as bk\n"
