@@ -32,6 +32,10 @@ struct Philox {
   }
 };
 
+// the 53-bit integer numpy's random() builds from two words (exact in f64)
+__device__ __forceinline__ double u53_int(uint32_t a, uint32_t b) {
+  return (double)(a >> 5) * 67108864.0 + (double)(b >> 6);
+}
 __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
   return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
 }
