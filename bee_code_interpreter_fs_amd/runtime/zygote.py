@@ -50,6 +50,11 @@ def _site_dirs_without_hooks() -> None:
         return
     import site
 
+    # the builtins `site` adds (exit / quit, help, copyright / credits /
+    # license): scripts call exit() as in any interpreter
+    site.setquit()
+    site.setcopyright()
+    site.sethelper()
     dirs = []
     if site.check_enableusersite():
         dirs.append(site.getusersitepackages())

@@ -237,3 +237,11 @@ def test_beekern_only_script_runs_numpy_free(stub):
     r = stub.Execute(pb.ExecuteRequest(source_code="import sys\nimport numpy, beekern\nprint('numpy' in sys.modules)\n"),
                      timeout=120)
     assert (r.exit_code, r.stdout) == (0, "True\n"), r.stderr
+
+
+def test_stdlib_only_script_has_the_site_builtins(stub):
+    """nano_cpu sandboxes come from a `python -S` zygote: exit() / quit() and
+    the other builtins `site` would add still exist."""
+    r = stub.Execute(pb.ExecuteRequest(source_code="import sys\nprint(sys.flags.no_site, callable(help))\nexit(3)\n"),
+                     timeout=120)
+    assert (r.exit_code, r.stdout) == (3, "1 True\n"), (r.stdout, r.stderr)
