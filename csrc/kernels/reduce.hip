@@ -421,6 +421,12 @@ __global__ __launch_bounds__(256) void rowsum_v(const T* __restrict__ x, int64_t
   if (lane == 0) out[row] = (TO)(acc * scale);
 }
 
+inline int64_t env_int(const char* name, int64_t dflt) {
+  const char* e = getenv(name);
+  const long long v = e ? atoll(e) : 0;
+  return v > 0 ? (int64_t)v : dflt;
+}
+
 template <typename T, typename TO>
 int launch_axis(const T* x, int64_t rows, int64_t cols, int64_t ld, int axis, TO* out, double scale, double* ws,
                 hipStream_t s) {
@@ -437,12 +443,17 @@ int launch_axis(const T* x, int64_t rows, int64_t cols, int64_t ld, int axis, TO
   const bool vec = cols % V == 0 && ld % V == 0 && ((uintptr_t)x & 15) == 0 &&
                    (cols + 16 * V - 1) / (16 * V) <= kAxisTickets;
   const int64_t col_blocks = vec ? (cols + 16 * V - 1) / (16 * V) : (cols + 255) / 256;
-  // enough row chunks for ~1k blocks, as far as the workspace allows; each
-  // chunk at least 32 rows so a lane streams several vectors (vec: 128 rows,
-  // two 64-row steps of the 16-wave block)
-  int64_t chunks = 1024 / col_blocks;
+  // row chunks: the scalar kernel aims at ~1k blocks of >= 32 rows; the
+  // 16-wave vector kernel at ~256 blocks of >= 512 rows (a block that streams
+  // only 2 steps is mostly block start-up, ticket and fold: 4096^2 bf16 ran
+  // 16 us in 1024 blocks of 128 rows while 4x the rows in the same 1024
+  // blocks ran 23 us, tools/probe/axis_shapes.py).  BK_COLSUM_BLOCKS /
+  // BK_COLSUM_MIN_ROWS override the vector targets (lab sweeps).
+  static const int64_t vec_blocks = env_int("BK_COLSUM_BLOCKS", 256);
+  static const int64_t vec_min_rows = env_int("BK_COLSUM_MIN_ROWS", 512);
+  int64_t chunks = (vec ? vec_blocks : 1024) / col_blocks;
   if (chunks * cols > kAxisWsDoubles) chunks = kAxisWsDoubles / cols;
-  const int64_t min_rows = vec ? 128 : 32;
+  const int64_t min_rows = vec ? vec_min_rows : 32;
   if (chunks > (rows + min_rows - 1) / min_rows) chunks = (rows + min_rows - 1) / min_rows;
   if (chunks < 1) chunks = 1;
   const int64_t per = (rows + chunks - 1) / chunks;
