@@ -444,13 +444,14 @@ int launch_axis(const T* x, int64_t rows, int64_t cols, int64_t ld, int axis, TO
                    (cols + 16 * V - 1) / (16 * V) <= kAxisTickets;
   const int64_t col_blocks = vec ? (cols + 16 * V - 1) / (16 * V) : (cols + 255) / 256;
   // row chunks: the scalar kernel aims at ~1k blocks of >= 32 rows; the
-  // 16-wave vector kernel at ~256 blocks of >= 512 rows (a block that streams
-  // only 2 steps is mostly block start-up, ticket and fold: 4096^2 bf16 ran
-  // 16 us in 1024 blocks of 128 rows while 4x the rows in the same 1024
-  // blocks ran 23 us, tools/probe/axis_shapes.py).  BK_COLSUM_BLOCKS /
-  // BK_COLSUM_MIN_ROWS override the vector targets (lab sweeps).
-  static const int64_t vec_blocks = env_int("BK_COLSUM_BLOCKS", 256);
-  static const int64_t vec_min_rows = env_int("BK_COLSUM_MIN_ROWS", 512);
+  // 16-wave vector kernel at ~128 blocks of >= 1024 rows (a block that
+  // streams only 2 steps is mostly block start-up, ticket and fold).  4096^2
+  // bf16, rocprofv3 min: 1024 blocks x 128 rows 14.2 us, 256 x 512 10.6,
+  // 128 x 1024 9.4 (profiles/r3_colsum_chunking_sweep.log,
+  // tools/probe/axis_shapes.py).  BK_COLSUM_BLOCKS / BK_COLSUM_MIN_ROWS
+  // override the vector targets (lab sweeps).
+  static const int64_t vec_blocks = env_int("BK_COLSUM_BLOCKS", 128);
+  static const int64_t vec_min_rows = env_int("BK_COLSUM_MIN_ROWS", 1024);
   int64_t chunks = (vec ? vec_blocks : 1024) / col_blocks;
   if (chunks * cols > kAxisWsDoubles) chunks = kAxisWsDoubles / cols;
   const int64_t min_rows = vec ? vec_min_rows : 32;
