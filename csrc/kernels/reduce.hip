@@ -482,8 +482,12 @@ BK_API int bk_rand_reduce(int op, int dtype, int64_t n, uint64_t seed, uint64_t 
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const int64_t units = dtype == kF64 ? (n + 1) / 2 : (n + 3) / 4;
   // fixed grid for a given n: results are reproducible run to run
-  unsigned g = stream_grid(units > 0 ? (units + 7) / 8 : 1, kRedBlock, kRandRedMaxBlocks / kNumCU);
-  if (g > (unsigned)kRandRedMaxBlocks) g = kRandRedMaxBlocks;
+  // (BK_RANDRED_BLOCKS: lab override of the grid cap, <= kRedMaxBlocks)
+  static const int64_t max_blocks = env_int("BK_RANDRED_BLOCKS", kRandRedMaxBlocks) <= kRedMaxBlocks
+                                        ? env_int("BK_RANDRED_BLOCKS", kRandRedMaxBlocks)
+                                        : kRandRedMaxBlocks;
+  unsigned g = stream_grid(units > 0 ? (units + 7) / 8 : 1, kRedBlock, (int)(max_blocks / kNumCU));
+  if (g > (unsigned)max_blocks) g = (unsigned)max_blocks;
   double* ws = (double*)workspace;
   unsigned* t = reinterpret_cast<unsigned*>(ws + kRedMaxBlocks);
   double* o = (double*)out;
