@@ -245,3 +245,19 @@ def test_stdlib_only_script_has_the_site_builtins(stub):
     r = stub.Execute(pb.ExecuteRequest(source_code="import sys\nprint(sys.flags.no_site, callable(help))\nexit(3)\n"),
                      timeout=120)
     assert (r.exit_code, r.stdout) == (3, "1 True\n"), (r.stdout, r.stderr)
+
+
+def test_repeated_source_runs_precompiled_with_the_same_traceback(stub):
+    """The second Execute of the same source gets the front-end's
+    precompiled code (scheduler/local_gpu_pool.py precompiled_if_repeated):
+    output, exit status and the traceback (file name, line, source line)
+    are the ones the sandbox's own compile gives."""
+    src = "import os\n\ndef f(x):\n    return 1 / x\n\nprint('before', __name__)\nf(0)\n"
+    runs = [stub.Execute(pb.ExecuteRequest(source_code=src), timeout=120) for _ in range(3)]
+    for r in runs:
+        assert r.exit_code == 1 and r.stdout == "before __main__\n", (r.stdout, r.stderr)
+        assert 'line 7, in <module>' in r.stderr and 'line 4, in f' in r.stderr, r.stderr
+        assert "return 1 / x" in r.stderr and "ZeroDivisionError" in r.stderr, r.stderr
+    # same frames, same file, whichever way the code was compiled
+    strip = lambda e: [l for l in e.splitlines() if "File " not in l]  # noqa: E731 - tmp script names differ
+    assert strip(runs[0].stderr) == strip(runs[1].stderr) == strip(runs[2].stderr)
