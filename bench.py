@@ -114,6 +114,8 @@ def parse_args():
     # warm-up steps ran at 1836 RPS vs ~2700 sustained, profiles/archive/r2_s3_bench_suite.jsonl)
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--concurrency", type=int, default=8, help="closed-loop clients per GPU")
+    p.add_argument("--clients-per-loadgen", type=int, default=0,
+                   help="clients per load-generator process (single-process runs; 0 = all of a GPU's clients in one)")
     p.add_argument("--pool-target", type=int, default=16, help="warm minimal sandboxes per GPU")
     p.add_argument("--frontends", type=int, default=0, help="front-end replicas (0 = three per GPU, at most 16)")
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="numpy_gpu")
@@ -617,7 +619,11 @@ def main():
         first = rank * args.concurrency
         # offered load: `concurrency` clients per GPU.  torchrun ranks are one
         # load generator each; a single-process N-GPU run starts N of them.
-        loadgens = n_gpus if world == 1 and n_gpus > 1 else 1
+        per_lg = args.clients_per_loadgen if 0 < args.clients_per_loadgen < args.concurrency else args.concurrency
+        lg_per_gpu = -(-args.concurrency // per_lg)
+        loadgens = n_gpus * lg_per_gpu if world == 1 and (n_gpus > 1 or lg_per_gpu > 1) else 1
+        if loadgens == 1:
+            per_lg = args.concurrency
 
         if rank == 0:
             wait_pools_ready(hport)
@@ -627,7 +633,7 @@ def main():
         svc_pid = proc.pid if proc is not None else None
         if loadgens > 1:
             marks = {"roles0": None, "svc": svc_pid}
-            gathered = run_loadgens(loadgens, targets, source, args.concurrency, args.warmup, args.steps, barrier, marks)
+            gathered = run_loadgens(loadgens, targets, source, per_lg, args.warmup, args.steps, barrier, marks)
             elapsed = max(g[0] for g in gathered)
             cpu_busy = (cpu_usage_s()[0] - marks["cpu0"]) / max(time.perf_counter() - marks["t0"], 1e-9)
             roles0, roles1 = marks["roles0"], marks.get("roles1")
@@ -660,7 +666,7 @@ def main():
         if args.workload == "numpy_gpu" and mat_steps > 0 and not args.payload:
             msrc = open(MATERIALIZED).read()
             if loadgens > 1:
-                mg = run_loadgens(loadgens, targets, msrc, args.concurrency, 1, mat_steps, barrier)
+                mg = run_loadgens(loadgens, targets, msrc, per_lg, 1, mat_steps, barrier)
             else:
                 loop.run_until_complete(run_clients(stubs, msrc, 1))
                 barrier()
@@ -697,7 +703,7 @@ def main():
                 else None
             )
             total = len(all_lat)
-            clients = args.concurrency * max(world, loadgens)
+            clients = per_lg * loadgens if world == 1 else args.concurrency * world
             pods = 1 if args.cpu_only else len(gpu_ids(n_gpus, args))
             kind = "CPU-only" if args.cpu_only else "virtual-GPU (CPU rehearsal)" if args.virtual_gpus else "GPU-pinned"
             out = {
