@@ -379,9 +379,12 @@ async def run_clients(stubs, source, n, trace=None):
     return out
 
 
-def _loadgen_main(targets, first, source, concurrency, warmup, steps, barrier, results):
+def _loadgen_main(targets, first, source, concurrency, warmup, steps, barrier, results, go=None):
     """One load-generator process (single-process ``--gpus N`` runs start N
-    of them, so offered load grows with N like the torchrun ranks do)."""
+    of them, so offered load grows with N like the torchrun ranks do).
+    ``barrier``: every load generator of this process tree has warmed up;
+    ``go``: the parent has also synchronised with the other ranks -- the
+    timed window starts on every rank at once."""
     sys.path.insert(0, ROOT)
     loop = asyncio.new_event_loop()
     chans = []
@@ -389,11 +392,15 @@ def _loadgen_main(targets, first, source, concurrency, warmup, steps, barrier, r
         chans, stubs = loop.run_until_complete(open_clients(targets, first, concurrency))
         loop.run_until_complete(run_clients(stubs, source, warmup))
         barrier.wait()
+        if go is not None:
+            go.wait()
         t0 = time.perf_counter()
         lat, errors, exec_times, phases = loop.run_until_complete(run_clients(stubs, source, steps))
         results.put((time.perf_counter() - t0, lat, errors, exec_times, phases))
     except BaseException as e:  # noqa: BLE001 - report instead of hanging the barrier
         barrier.abort()
+        if go is not None:
+            go.abort()
         results.put((0.0, [], [f"loadgen failed: {e!r}"[:300]], [], {}))
     finally:
         if chans:
@@ -401,24 +408,29 @@ def _loadgen_main(targets, first, source, concurrency, warmup, steps, barrier, r
         loop.close()
 
 
-def run_loadgens(n_procs, targets, source, concurrency, warmup, steps, sync, marks=None):
+def run_loadgens(n_procs, targets, source, concurrency, warmup, steps, sync, marks=None, first=0):
     """``n_procs`` client processes of ``concurrency`` clients each; times
     the steps between one barrier all of them (and this process) pass and
     their completion.  Returns the gathered tuples (elapsed per process)."""
     import multiprocessing as mp
 
     ctx = mp.get_context("spawn")
-    barrier = ctx.Barrier(n_procs + 1)
+    barrier, go = ctx.Barrier(n_procs + 1), ctx.Barrier(n_procs + 1)
     results = ctx.Queue()
-    procs = [ctx.Process(target=_loadgen_main, args=(targets, i * concurrency, source, concurrency, warmup, steps,
-                                                     barrier, results), daemon=True) for i in range(n_procs)]
+    procs = [ctx.Process(target=_loadgen_main, args=(targets, first + i * concurrency, source, concurrency, warmup,
+                                                     steps, barrier, results, go), daemon=True)
+             for i in range(n_procs)]
     for p in procs:
         p.start()
     try:
         barrier.wait(timeout=900)
     except Exception:  # a load generator failed during warm-up
         pass
-    sync()
+    sync()  # every rank's load generators warmed up (torchrun: a dist barrier)
+    try:
+        go.wait(timeout=900)
+    except Exception:
+        pass
     if marks is not None:
         marks["t0"], marks["cpu0"] = time.perf_counter(), cpu_usage_s()[0]
         marks["roles0"] = cpu_by_role(marks.get("svc"))
@@ -617,13 +629,23 @@ def main():
         target = f"127.0.0.1:{gport}"
         targets = replicas or [target]
         first = rank * args.concurrency
-        # offered load: `concurrency` clients per GPU.  torchrun ranks are one
-        # load generator each; a single-process N-GPU run starts N of them.
+        # offered load: `concurrency` clients per GPU.  A torchrun rank drives
+        # its GPU's clients, a single-process N-GPU run all N GPUs'; either
+        # in this process, or over load-generator processes of
+        # --clients-per-loadgen clients each (every rank the same way, so the
+        # per-GPU client setup does not change with N)
         per_lg = args.clients_per_loadgen if 0 < args.clients_per_loadgen < args.concurrency else args.concurrency
         lg_per_gpu = -(-args.concurrency // per_lg)
-        loadgens = n_gpus * lg_per_gpu if world == 1 and (n_gpus > 1 or lg_per_gpu > 1) else 1
+        loadgens = (n_gpus if world == 1 else 1) * lg_per_gpu
         if loadgens == 1:
             per_lg = args.concurrency
+
+        def gather_ranks(local):  # every rank's load-generator tuples, on every rank
+            if world == 1:
+                return local
+            allg = [None] * world
+            dist.all_gather_object(allg, local)
+            return [g for part in allg for g in part]
 
         if rank == 0:
             wait_pools_ready(hport)
@@ -633,7 +655,8 @@ def main():
         svc_pid = proc.pid if proc is not None else None
         if loadgens > 1:
             marks = {"roles0": None, "svc": svc_pid}
-            gathered = run_loadgens(loadgens, targets, source, per_lg, args.warmup, args.steps, barrier, marks)
+            gathered = gather_ranks(run_loadgens(loadgens, targets, source, per_lg, args.warmup, args.steps, barrier,
+                                                 marks, first=first))
             elapsed = max(g[0] for g in gathered)
             cpu_busy = (cpu_usage_s()[0] - marks["cpu0"]) / max(time.perf_counter() - marks["t0"], 1e-9)
             roles0, roles1 = marks["roles0"], marks.get("roles1")
@@ -666,7 +689,7 @@ def main():
         if args.workload == "numpy_gpu" and mat_steps > 0 and not args.payload:
             msrc = open(MATERIALIZED).read()
             if loadgens > 1:
-                mg = run_loadgens(loadgens, targets, msrc, per_lg, 1, mat_steps, barrier)
+                mg = gather_ranks(run_loadgens(loadgens, targets, msrc, per_lg, 1, mat_steps, barrier, first=first))
             else:
                 loop.run_until_complete(run_clients(stubs, msrc, 1))
                 barrier()
@@ -703,7 +726,7 @@ def main():
                 else None
             )
             total = len(all_lat)
-            clients = per_lg * loadgens if world == 1 else args.concurrency * world
+            clients = per_lg * loadgens * world
             pods = 1 if args.cpu_only else len(gpu_ids(n_gpus, args))
             kind = "CPU-only" if args.cpu_only else "virtual-GPU (CPU rehearsal)" if args.virtual_gpus else "GPU-pinned"
             out = {
@@ -726,7 +749,7 @@ def main():
                     "global_batch": clients,
                     "seq_len": None,
                     "parallelism": f"{pods} {kind} executor pods, {frontends} front-end replicas, "
-                    f"{clients} concurrent clients ({args.concurrency} per GPU, {max(world, loadgens)} load-generator processes)"
+                    f"{clients} concurrent clients ({args.concurrency} per GPU, {max(world, loadgens * world)} load-generator processes)"
                     + (f" (round-robin over the {len(replicas)} replica ports)" if replicas else ""),
                     "execution": "every Execute runs in its own single-use sandbox process on the pinned GPU; "
                     "beekern draws are lazy, so sum(square(rand(1e8))) lowers to one fused Philox->square->reduce "
