@@ -278,8 +278,10 @@ int main(int argc, char** argv) {
     }
     if (req.method == "POST" && (p == "/v1/execute" || p == "/execute")) {
       Json body;
+      CpuLap parse_lap;
       try {
         body = Json::parse(req.body->read_all(256 << 20));
+        parse_lap.lap(kCpuJobParse);
       } catch (const std::exception& e) {
         resp.error(422, std::string("invalid JSON body: ") + e.what());
         return;
@@ -290,7 +292,9 @@ int main(int argc, char** argv) {
       }
       int code = 200;
       Json out = (p == "/execute" || pool.config().pod_mode) ? pool.execute_pod(body, &code) : pool.execute(body, &code);
+      CpuLap dump_lap;
       resp.json(code, out.dump());
+      dump_lap.lap(kCpuJobRespond);
       return;
     }
     if (pool.config().pod_mode && (req.method == "PUT" || req.method == "GET") &&

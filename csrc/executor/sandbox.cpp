@@ -235,6 +235,7 @@ bool SandboxPool::start(std::string* err) {
   }
   acceptor_thread_ = std::thread([this] { worker_acceptor(); });
   cleanup_thread_ = std::thread([this] { cleanup_loop(); });
+  refill_thread_ = std::thread([this] { refill_loop(); });
   const bool watch_hbm = cfg_.hbm_watchdog_ms > 0 && !cfg_.gpus.empty();
   const bool contain = cfg_.sandbox_mem_bytes > 0 || cfg_.sandbox_tasks > 0 || cfg_.sandbox_cpus > 0;
   if (watch_hbm || contain) watchdog_thread_ = std::thread([this] { watchdog_loop(); });
@@ -285,6 +286,11 @@ void SandboxPool::stop() {
   unlink(worker_sock_path_.c_str());
   cv_.notify_all();
   cleanup_cv_.notify_all();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    refill_cv_.notify_all();
+  }
+  if (refill_thread_.joinable()) refill_thread_.join();
   for (auto& z : zygotes_)
     if (z->thread.joinable()) z->thread.join();
   if (acceptor_thread_.joinable()) acceptor_thread_.join();
@@ -566,7 +572,7 @@ void SandboxPool::zygote_reader(Zygote* z) {
     } else if (op == "log") {
       BEE_INFO("zygote: %s", m["msg"].as_string().c_str());
     }
-    if (!stopping_) refill_locked();
+    if (!stopping_) request_refill_locked();
     lk.unlock();
     cv_.notify_all();
     cleanup_cv_.notify_all();
@@ -814,6 +820,17 @@ std::shared_ptr<Worker> SandboxPool::spawn_worker(bool pooled, int kind, const s
   return w;
 }
 
+void SandboxPool::refill_loop() {
+  ThreadRoleScope role(kThrRefill);
+  std::unique_lock<std::mutex> lk(mu_);
+  while (!stopping_) {
+    refill_cv_.wait(lk, [this] { return refill_wanted_ || stopping_; });
+    if (stopping_) break;
+    refill_wanted_ = false;
+    refill_locked();
+  }
+}
+
 void SandboxPool::refill_locked() {
   if (stopping_ || !any_zygote_alive()) return;
   // release queued (direct) spawns as slots free up
@@ -953,7 +970,7 @@ void SandboxPool::worker_acceptor() {
         }
         if (!m["gpu_error"].as_string().empty())
           BEE_WARN("worker %s: GPU warm-up failed: %s", w->id.c_str(), m["gpu_error"].as_string().c_str());
-        refill_locked();
+        request_refill_locked();
       }
     } else if (op == "done") {
       w->done = true;
@@ -1066,10 +1083,10 @@ std::shared_ptr<Worker> SandboxPool::acquire(int kind, double timeout_s, std::st
       ready.pop_front();
       if (w->exited || w->fd < 0) continue;
       w->state = WorkerState::Running;
-      refill_locked();
+      request_refill_locked();
       return w;
     }
-    refill_locked();
+    request_refill_locked();
     if (stopping_) {
       *err = "executor stopping";
       return nullptr;
@@ -1372,6 +1389,7 @@ static Json timings_json(const ExecTimings& t) {
 
 Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   const double t0 = mono_ms();
+  CpuLap cpu_lap;
   ExecTimings tm;
   *http_status = 200;
   auto fail = [&](int code, const std::string& detail) {
@@ -1444,6 +1462,7 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
     publish_load_locked();
   }
   cv_.notify_all();  // the next ticket may fit as well
+  cpu_lap.lap(kCpuJobAdmit);
   struct JobGuard {
     SandboxPool* p;
     int64_t hbm;
@@ -1540,6 +1559,7 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   }
   auto lead = ranks[0];
   tm.acquire_ms = mono_ms() - t0;
+  cpu_lap.lap(kCpuJobAcquire);
   auto cleanup_all = [&]() {
     for (auto& w : ranks) destroy(w);
   };
@@ -1589,6 +1609,7 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   }
   auto before = scan_files(lead->ws, cfg_.recursive_scan);
   tm.stage_ms = mono_ms() - t1;
+  cpu_lap.lap(kCpuJobStage);
 
   // 3. run
   const double t2 = mono_ms();
@@ -1685,6 +1706,7 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   // sandbox's UID must not touch the workspace while it is collected
   if (lead->uid) sweep_uid(lead->uid, false);
   tm.run_ms = mono_ms() - t2;
+  cpu_lap.lap(kCpuJobRun);
 
   // 4. collect outputs
   const double t3 = mono_ms();
@@ -1756,7 +1778,9 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   tm.collect_ms = mono_ms() - t3;
   bool tj_trunc = false;
   const std::string timing_text = read_file_capped(join_path(lead->meta, "timing.json"), 4096, &tj_trunc);
+  cpu_lap.lap(kCpuJobCollect);
   cleanup_all();
+  cpu_lap.lap(kCpuJobCleanup);
   tm.total_ms = mono_ms() - t0;
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -1798,6 +1822,7 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   resp.set("worker", lead->id);
   resp.set("gpus", lead->gpus);
   resp.set("warm_ms", lead->warm_ms);
+  cpu_lap.lap(kCpuJobRespond);
   return resp;
 }
 

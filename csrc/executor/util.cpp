@@ -20,11 +20,13 @@
 namespace bee {
 
 std::atomic<int64_t> g_cpu_ns[kCpuParts];
-const char* const kCpuPartNames[kCpuParts] = {"http", "worker_io", "zygote_io", "broker", "cleanup"};
+const char* const kCpuPartNames[kCpuParts] = {"http",        "worker_io",  "zygote_io",   "broker",    "cleanup",
+                                              "job_parse",   "job_admit",  "job_acquire", "job_stage", "job_run",
+                                              "job_collect", "job_cleanup", "job_respond"};
 std::atomic<int64_t> g_thread_exit_ns[kThrRoles];
 // thread names (comm, <= 15 chars): what /proc/self/task/*/comm shows
 const char* const kThreadRoleNames[kThrRoles] = {"bee-http", "bee-wreader", "bee-zreader", "bee-broker",
-                                                 "bee-accept", "bee-cleanup", "bee-watchdog"};
+                                                 "bee-accept", "bee-cleanup", "bee-watchdog", "bee-refill"};
 
 ThreadRoleScope::ThreadRoleScope(ThreadRole r) : role(r) { pthread_setname_np(pthread_self(), kThreadRoleNames[r]); }
 

@@ -25,7 +25,9 @@ double mono_ms();      // CLOCK_MONOTONIC, milliseconds
 // ---- CPU accounting ---------------------------------------------------------
 // Thread CPU time spent per daemon role, exported on /metrics and /v1/status
 // (which part of the per-request CPU budget the daemon itself costs).
-enum CpuPart { kCpuHttp = 0, kCpuWorkerIo, kCpuZygoteIo, kCpuBroker, kCpuCleanup, kCpuParts };
+// (kCpuJob*: the /v1/execute handler's phases, a breakdown of kCpuHttp)
+enum CpuPart { kCpuHttp = 0, kCpuWorkerIo, kCpuZygoteIo, kCpuBroker, kCpuCleanup, kCpuJobParse, kCpuJobAdmit,
+               kCpuJobAcquire, kCpuJobStage, kCpuJobRun, kCpuJobCollect, kCpuJobCleanup, kCpuJobRespond, kCpuParts };
 extern std::atomic<int64_t> g_cpu_ns[kCpuParts];
 extern const char* const kCpuPartNames[kCpuParts];
 inline int64_t thread_cpu_ns() {
@@ -33,6 +35,16 @@ inline int64_t thread_cpu_ns() {
   clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
   return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
 }
+// consecutive phases of one thread's work: lap(p) charges the CPU since the
+// previous lap to part p
+struct CpuLap {
+  int64_t t = thread_cpu_ns();
+  void lap(CpuPart p) {
+    const int64_t n = thread_cpu_ns();
+    g_cpu_ns[p] += n - t;
+    t = n;
+  }
+};
 struct CpuScope {
   CpuPart part;
   int64_t t0;
@@ -46,7 +58,7 @@ struct CpuScope {
 // process total minus these is what threads we did not start cost (the HIP
 // runtime's, in a daemon with a kernel broker).
 enum ThreadRole { kThrHttp = 0, kThrWorkerReader, kThrZygoteReader, kThrBrokerPool, kThrAcceptor, kThrCleanup,
-                  kThrWatchdog, kThrRoles };
+                  kThrWatchdog, kThrRefill, kThrRoles };
 extern std::atomic<int64_t> g_thread_exit_ns[kThrRoles];
 extern const char* const kThreadRoleNames[kThrRoles];
 struct ThreadRoleScope {
