@@ -135,6 +135,13 @@ enum WorkerKind { kDirect = 0, kLight = 1, kMin = 2, kMinCpu = 3, kNano = 4, kNa
 enum class WorkerState { Spawning, Connected, Ready, Running, Exited, Failed };
 
 struct Worker {
+  // the running job's wake-up: its request thread waits on this (with the
+  // pool's mutex) for "done" / exit, instead of on the pool-wide condition
+  // every spawn, ready and exit of every sandbox notifies
+  std::shared_ptr<std::condition_variable> job_cv;
+  void notify_job() const {
+    if (job_cv) job_cv->notify_all();
+  }
   std::string id;
   std::string dir, ws, rp, meta;
   std::string gpus;
