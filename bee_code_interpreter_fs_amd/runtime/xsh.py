@@ -359,11 +359,39 @@ def translate(source: str) -> Optional[str]:
     return assemble(is_shell)
 
 
+def _valid_python_needs_lowering(source: str) -> bool:
+    """The screen passed (a `$` in a string, a docstring line that reads like
+    a command, ...): one parse of the whole payload settles most cases.  A
+    payload that is valid Python has no xonsh operator outside its strings
+    (`$`, `!(`, `![` are syntax errors there), so only a bare-name
+    expression statement (`pwd`, `ls -la`) whose leading name the script
+    never binds can still be a command; the per-line analysis runs only
+    then, or when the payload is not Python at all."""
+    try:
+        tree = ast.parse(source)
+    except (SyntaxError, ValueError, RecursionError, MemoryError):
+        return True
+    candidates = []
+    for node in ast.walk(tree):
+        if isinstance(node, ast.Expr):
+            name = _leftmost_name(node.value)
+            if name is not None and name not in _PY_NAMES:
+                candidates.append(name)
+        elif isinstance(node, ast.alias) and node.name == "*":
+            return False  # names no scan can see: bare names stay Python
+    if not candidates:
+        return False
+    bound = _bound_names(tree)
+    return any(n not in bound for n in candidates)
+
+
 def lower_payload(source: str) -> Optional[str]:
     """The payload's lowering, or None when it is plain Python (or its
     lowering would not compile either: the original text's SyntaxError is
     then the report)."""
     if not maybe_shell(source):
+        return None
+    if not _valid_python_needs_lowering(source):
         return None
     try:
         lowered = translate(source)

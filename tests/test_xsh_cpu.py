@@ -221,3 +221,15 @@ def test_shell_payload_through_service(stub):
     assert r.exit_code == 0, r.stderr
     assert r.stdout.splitlines() == ["cwd /workspace", "hello from the shell", "True", "rc True"], r.stdout
     assert set(r.files) == {"/workspace/note.txt"}
+
+
+def test_docstring_heavy_python_is_screened_by_one_parse():
+    """Lines inside strings can look like commands to the line screen; a
+    payload that parses as Python with no unbound bare-name statement is
+    settled by one parse, not the per-line analysis."""
+    src = 'def f(x):\n    """This function does things\n    and more things"""\n    return x\n' * 50
+    assert xsh.maybe_shell(src)  # the screen alone cannot tell
+    assert not xsh._valid_python_needs_lowering(src)
+    assert xsh.lower_payload(src) is None
+    assert xsh._valid_python_needs_lowering("x = 1\nls -la\n")  # unbound bare name: a command
+    assert xsh._valid_python_needs_lowering("echo $HOME\n")  # not Python at all
