@@ -227,7 +227,7 @@ def test_docstring_heavy_python_is_screened_by_one_parse():
     """Lines inside strings can look like commands to the line screen; a
     payload that parses as Python with no unbound bare-name statement is
     settled by one parse, not the per-line analysis."""
-    src = 'def f(x):\n    """This function does things\n    and more things"""\n    return x\n' * 50
+    src = 'def f(x):\n    """Return x.\n\n    Compute the value\n    """\n    return x\n' * 50
     assert xsh.maybe_shell(src)  # the screen alone cannot tell
     assert not xsh._valid_python_needs_lowering(src)
     assert xsh.lower_payload(src) is None
