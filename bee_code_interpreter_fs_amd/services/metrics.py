@@ -47,18 +47,23 @@ class Metrics:
             h.observe(value_ms)
 
     def observe_phases(self, name: str, timings_ms: dict, label: str = "phase") -> None:
-        """observe_ms for every (phase, ms) of one request under one lock,
-        with the label keys cached (called on every Execute)."""
+        """observe_ms for every (phase, ms) of one request under one lock:
+        one cached lookup per phase straight to its histogram, the update
+        inlined (called on every Execute, ~20 phases each)."""
         cache = self._phase_keys
+        bl = bisect.bisect_left
         with self._lock:
             for phase, ms in timings_ms.items():
-                key = cache.get((name, label, phase))
-                if key is None:
-                    key = cache[(name, label, phase)] = (name, ((label, phase),))
-                h = self.hists.get(key)
+                h = cache.get((name, label, phase))
                 if h is None:
-                    h = self.hists[key] = Histogram()
-                h.observe(ms)
+                    key = (name, ((label, phase),))
+                    h = self.hists.get(key)
+                    if h is None:
+                        h = self.hists[key] = Histogram()
+                    cache[(name, label, phase)] = h
+                h.counts[bl(_BUCKETS_MS, ms)] += 1
+                h.total += ms
+                h.n += 1
 
     def render(self) -> str:
         lines = []
