@@ -12,15 +12,29 @@
 namespace bk {
 
 // out[i] = U[0,1) (f64), scaled to [lo, hi).  Each counter value -> 2 doubles.
+// lo + span * u as one fma of the 53-bit integer (span * 2^-53 is exact: the
+// same bits as rand_reduce_f64's fused draw, one f64 multiply fewer), and two
+// counters per lane per iteration so two Philox chains overlap the stores.
 template <bool NT>
 __global__ __launch_bounds__(256) void philox_uniform_f64(double* __restrict__ out, int64_t n, uint32_t k0,
                                                           uint32_t k1, uint64_t offset, double lo, double span) {
-  const int64_t pairs = (n + 1) / 2;
+  const int64_t pairs = (n + 1) / 2, full = n / 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < pairs; p += stride) {
+  const double s53 = span * (1.0 / 9007199254740992.0);
+  int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; p + stride < full; p += 2 * stride) {
+    const uint64_t c0 = offset + (uint64_t)p, c1 = c0 + (uint64_t)stride;
+    const uint4 r0 = Philox::run(make_uint4((uint32_t)c0, (uint32_t)(c0 >> 32), kTagUniformF64, 0u), k0, k1);
+    const uint4 r1 = Philox::run(make_uint4((uint32_t)c1, (uint32_t)(c1 >> 32), kTagUniformF64, 0u), k0, k1);
+    st16<NT>(reinterpret_cast<double2*>(out + 2 * p),
+             make_double2(fma(u53_int(r0.x, r0.y), s53, lo), fma(u53_int(r0.z, r0.w), s53, lo)));
+    st16<NT>(reinterpret_cast<double2*>(out + 2 * (p + stride)),
+             make_double2(fma(u53_int(r1.x, r1.y), s53, lo), fma(u53_int(r1.z, r1.w), s53, lo)));
+  }
+  for (; p < pairs; p += stride) {
     const uint64_t ctr = offset + (uint64_t)p;
     const uint4 r = Philox::run(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), kTagUniformF64, 0u), k0, k1);
-    double2 v = make_double2(lo + span * u53(r.x, r.y), lo + span * u53(r.z, r.w));
+    double2 v = make_double2(fma(u53_int(r.x, r.y), s53, lo), fma(u53_int(r.z, r.w), s53, lo));
     const int64_t i = 2 * p;
     if (i + 1 < n) {
       st16<NT>(reinterpret_cast<double2*>(out + i), v);  // 16-B store
@@ -132,9 +146,14 @@ BK_API int bk_rand_uniform(void* out, int64_t n, int dtype, uint64_t seed, uint6
   if (!out || n < 0) return kBadArgument;
   if (n == 0) return kOk;
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  // the f64 / f32 draws take a 4x larger grid cap than the elementwise
+  // kernels: 1e8 f64 (800 MB), rocprofv3 mean / min: 64 blocks/CU 146 / 139
+  // us, 128: 133 / 118, 256: 133 / 121, 512: 130 / 115
+  // (profiles/r3_philox_grid_sweep.log)
+  constexpr int kDrawBlocksPerCU = 256;
   if (dtype == kF64) {
     const int64_t pairs = (n + 1) / 2;
-    const unsigned g = stream_grid(pairs, 256);
+    const unsigned g = stream_grid(pairs, 256, kDrawBlocksPerCU);
     if (stream_nt(n * 8)) philox_uniform_f64<true><<<g, 256, 0, stream>>>((double*)out, n, k0, k1, offset, lo, hi - lo);
     else philox_uniform_f64<false><<<g, 256, 0, stream>>>((double*)out, n, k0, k1, offset, lo, hi - lo);
   } else if (dtype == kBF16) {
@@ -143,7 +162,7 @@ BK_API int bk_rand_uniform(void* out, int64_t n, int dtype, uint64_t seed, uint6
                                                                      (float)(hi - lo));
   } else if (dtype == kF32) {
     const int64_t quads = (n + 3) / 4;
-    const unsigned g = stream_grid(quads, 256);
+    const unsigned g = stream_grid(quads, 256, kDrawBlocksPerCU);
     if (stream_nt(n * 4))
       philox_uniform_f32<true><<<g, 256, 0, stream>>>((float*)out, n, k0, k1, offset, (float)lo, (float)(hi - lo));
     else

@@ -26,10 +26,20 @@ constexpr int kRedBlock = 256;
 // stage-1 grid cap, and the workspace length: 32 blocks per CU with 16 loads
 // in flight per lane (tools/probe/reduce_probe.hip: 1e8 f64 square-sum
 // 152 -> 120 us, 5.2 -> 6.6 TB/s, with non-temporal loads)
-constexpr int kRedMaxBlocks = 8192;
+// (the workspace holds kRedMaxBlocks partials; the default grid is
+// kRedBlocks, BK_REDUCE_BLOCKS overrides it up to the workspace for sweeps)
+constexpr int kRedMaxBlocks = 32768;
+constexpr int kRedBlocks = 8192;
 constexpr int kRedUnroll = 16;
 // the fused RNG->reduce kernels are compute-bound: 4 blocks per CU
 constexpr int kRandRedMaxBlocks = 1024;
+
+// lab overrides of grid targets (positive integers; anything else = default)
+inline int64_t env_int(const char* name, int64_t dflt) {
+  const char* e = getenv(name);
+  const long long v = e ? atoll(e) : 0;
+  return v > 0 ? (int64_t)v : dflt;
+}
 
 template <typename T> __device__ __forceinline__ double to_f64(T v);
 template <> __device__ __forceinline__ double to_f64<double>(double v) { return v; }
@@ -116,8 +126,19 @@ template <int OP>
 __device__ __forceinline__ void finish(double v, double* partials, unsigned* ticket, double* out) {
   if (threadIdx.x == 0) publish(partials + blockIdx.x, v);
   if (!take_last_ticket(ticket, gridDim.x)) return;
+  // 8 partial loads in flight per lane: they miss this XCD's L2, and one at
+  // a time the fold of 8192 partials (32 per lane) was a serial chain of
+  // memory latencies at the end of every reduction.  Fixed order per grid.
+  constexpr int F = 8;
+  const int count = (int)gridDim.x;
   double r = red_init<OP>();
-  for (int i = threadIdx.x; i < (int)gridDim.x; i += kRedBlock) r = red_combine<OP>(r, load_agent(partials + i));
+  for (int i = threadIdx.x; i < count; i += F * kRedBlock) {
+    double t[F];
+#pragma unroll
+    for (int u = 0; u < F; ++u) t[u] = i + u * kRedBlock < count ? load_agent(partials + i + u * kRedBlock) : red_init<OP>();
+#pragma unroll
+    for (int u = 0; u < F; ++u) r = red_combine<OP>(r, t[u]);
+  }
   r = block_reduce<OP>(r);
   if (threadIdx.x == 0) {
     *out = r;
@@ -149,6 +170,25 @@ __global__ __launch_bounds__(kRedBlock) void reduce_1pass(const T* __restrict__ 
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const double bj = kTwoOperands<OP> ? to_f64<T>(vb[u].v[j]) : 0.0;
+        acc[u] = red_combine<OP>(acc[u], red_map<OP>(to_f64<T>(va[u].v[j]), bj));
+      }
+  }
+  // the rest in groups of 4 loads in flight: at 1e8 f64 on the capped grid a
+  // lane has ~24 vectors, 16 + 8 -- one at a time, the last 8 cost as much
+  // as the first 16
+  constexpr int U2 = 4;
+  for (; i + (U2 - 1) * stride < nvec; i += U2 * stride) {
+    V va[U2], vb[U2];
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+      va[u] = ld16<NT>(reinterpret_cast<const V*>(a) + i + u * stride);
+      if constexpr (kTwoOperands<OP>) vb[u] = ld16<NT>(reinterpret_cast<const V*>(b) + i + u * stride);
+    }
+#pragma unroll
+    for (int u = 0; u < U2; ++u)
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         const double bj = kTwoOperands<OP> ? to_f64<T>(vb[u].v[j]) : 0.0;
@@ -241,8 +281,11 @@ template <typename T, int OP>
 int launch_reduce(const void* a, const void* b, int64_t n, double* workspace, double* out, hipStream_t s) {
   constexpr int N = 16 / sizeof(T);
   int64_t lanes_needed = (n / N + 3) / 4;  // 4 vectors per lane minimum before adding blocks
-  unsigned g = stream_grid(lanes_needed > 0 ? lanes_needed : 1, kRedBlock, kRedMaxBlocks / kNumCU);
-  if (g > (unsigned)kRedMaxBlocks) g = kRedMaxBlocks;  // the workspace holds kRedMaxBlocks partials
+  static const int64_t red_blocks = env_int("BK_REDUCE_BLOCKS", kRedBlocks) <= kRedMaxBlocks
+                                        ? env_int("BK_REDUCE_BLOCKS", kRedBlocks)
+                                        : kRedBlocks;
+  unsigned g = stream_grid(lanes_needed > 0 ? lanes_needed : 1, kRedBlock, (int)(red_blocks / kNumCU));
+  if (g > (unsigned)red_blocks) g = (unsigned)red_blocks;  // the workspace holds kRedMaxBlocks partials
   unsigned* ticket = reinterpret_cast<unsigned*>(workspace + kRedMaxBlocks);
   if (stream_nt(n * (int64_t)sizeof(T) * (kTwoOperands<OP> ? 2 : 1)))
     reduce_1pass<T, OP, true><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
@@ -419,12 +462,6 @@ __global__ __launch_bounds__(256) void rowsum_v(const T* __restrict__ x, int64_t
   }
   const double acc = wave_reduce<kRedSum>((a0 + a1) + (a2 + a3));
   if (lane == 0) out[row] = (TO)(acc * scale);
-}
-
-inline int64_t env_int(const char* name, int64_t dflt) {
-  const char* e = getenv(name);
-  const long long v = e ? atoll(e) : 0;
-  return v > 0 ? (int64_t)v : dflt;
 }
 
 template <typename T, typename TO>

@@ -61,6 +61,29 @@ def test_uniform_streams_match_host_philox_bitwise(gpu, n):
                                uniform_f32(n, seed, 0, -1.0, 1.0), rtol=0, atol=float(np.spacing(np.float32(2.0))))
 
 
+@pytest.mark.parametrize("n", [2 * 2 * 16384 * 256 + 12345, 40_000_003])
+def test_large_uniform_f64_windows_match_host_philox(gpu, n):
+    """Draws long enough for the f64 kernel's two-counters-per-lane loop
+    (the 40M draw's 20M pairs exceed one grid stride of 65536 x 256), its
+    one-counter tail, the odd last element, and (40M: 320 MB) the
+    non-temporal store path: windows at the start, across 4M-pair
+    boundaries and at the end equal the host reference stream bit for bit
+    (uniform_f64's offset is in pairs)."""
+    from .philox_ref import uniform_f64
+
+    seed = 0x0DDB_A11_5EED
+    x = gpu.random.default_rng(seed).random(n).numpy()
+    stride = 16384 * 256
+    w = 4096
+    pairs = (n + 1) // 2
+    for pair0 in [0, stride - w // 4, 2 * stride - w // 4, 3 * stride - w // 4, 4 * stride - w // 4, pairs - w // 2]:
+        if pair0 >= pairs:
+            continue
+        i0 = 2 * pair0
+        m = min(w, n - i0)
+        np.testing.assert_array_equal(x[i0:i0 + m], uniform_f64(m, seed, pair0), err_msg=f"window at {i0}")
+
+
 def test_fused_rand_square_sum_matches_host_reference(gpu):
     """The headline payload's lowering -- sum(square(rand(n))) as one fused
     Philox->square->reduce kernel -- against an fp64 host sum of the
@@ -140,6 +163,19 @@ def test_reductions(gpu, dtype, n):
     y = gpu.asarray(rng.standard_normal(n), dtype=dtype)
     ry = y.numpy().astype(np.float64)
     assert abs(gpu.dot(x, y) - (r * ry).sum()) <= rtol * (np.abs(r * ry).sum() + 1e-30)
+
+
+def test_reductions_long_array_all_loops(gpu):
+    """~1e8 f64 (805 MB, the materialised payload's size): on the capped grid
+    (8192 x 256 lanes) each lane takes ~24 vectors -- the 16-in-flight loop,
+    two 4-in-flight groups and the one-at-a-time tail all run; the odd
+    length leaves a scalar remainder."""
+    n = (1 << 26) + (1 << 25) + 12345
+    h = np.random.default_rng(11).random(n)
+    x = gpu.asarray(h)
+    assert abs(float(gpu.sum(x)) - h.sum()) <= 1e-12 * h.sum()
+    assert abs(float(gpu.square_sum(x)) - np.dot(h, h)) <= 1e-12 * np.dot(h, h)
+    assert float(gpu.amax(x)) == h.max()
 
 
 def test_reduction_is_deterministic(gpu):

@@ -42,7 +42,21 @@ def main():
     s = bk.sum(b, axis=0).astype("bfloat16").reshape(1, n)
     ref = bk.gemm_bf16_tn(a, s, out_dtype="float32").reshape(n)
     mb = 1 << 20
+    big = 10 ** 8
+    bk.set_lazy_random(False)
+    x = bk.random.rand(big)  # the materialised payload's 800 MB array
+    bk.set_lazy_random(True)
+
+    def rand_materialised():
+        prev = bk.set_lazy_random(False)
+        try:
+            return bk.random.rand(big)._materialize()
+        finally:
+            bk.set_lazy_random(prev)
+
     cases = [
+        ("philox_uniform f64 1e8 (materialised)", rand_materialised, 8 * big, None),
+        ("square-sum f64 1e8 (materialised array)", lambda: float(bk.sum(bk.square(x))), 8 * big, None),
         ("philox_uniform_bf16 4096^2", lambda: bk.random.uniform(-1, 1, (n, n), dtype="bfloat16"), 2 * n * n, None),
         ("gemm_bf16_tn 4096^3 (bf16 out)", lambda: bk.matmul(a, b.T), 3 * 2 * n * n, 2 * n ** 3),
         ("rand_reduce f64 1e8 square-sum", lambda: float(bk.sum(bk.square(bk.random.rand(10 ** 8)))), 0, None),
