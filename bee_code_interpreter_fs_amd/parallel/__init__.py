@@ -63,7 +63,9 @@ def init_process_group(backend: Optional[str] = None):
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl":
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    rdzv = os.environ.get("BEE_GANG_RDZV")
+    from ..runtime.sandbox_patches import next_rendezvous
+
+    rdzv = next_rendezvous()  # a fresh FileStore file per init
     if rdzv:
         dist.init_process_group(backend, init_method=rdzv, rank=rank, world_size=world)
     else:

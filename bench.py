@@ -333,7 +333,7 @@ async def close_clients(chans):
 
 
 async def client_loop(stub, pb, source, budget, out, trace=None):
-    lat, errors, exec_times, phases = out
+    lat, errors, exec_times, phases, checks = out
     while budget[0] > 0:
         budget[0] -= 1  # (one event loop: taken before the await, no race)
         t = time.perf_counter()
@@ -352,9 +352,11 @@ async def client_loop(stub, pb, source, budget, out, trace=None):
         try:
             if ok and "Result:" in r.stdout:  # benchmark-numpy payloads: check the math
                 ok = result_ok(float(r.stdout.split("Result:")[1].split()[0]))
+                checks["result_ok"] += ok
             if ok and "GEMM max row error:" in r.stdout:  # and every row of the GEMM
                 ok = gemm_row_ok(float(r.stdout.split("GEMM max row error:")[1].split()[0])) and \
                     abs(float(r.stdout.split("GEMM checksum:")[1].split()[0])) < 1e9
+                checks["gemm_ok"] += ok
             if ok and "Execution Time:" in r.stdout:
                 exec_times.append(float(r.stdout.split("Execution Time:")[1].split()[0]) * 1e3)
         except (IndexError, ValueError):
@@ -373,7 +375,7 @@ async def run_clients(stubs, source, n, trace=None):
     the offered concurrency."""
     from bee_code_interpreter_fs_amd.models import proto as pb
 
-    out = ([], [], [], {})
+    out = ([], [], [], {}, {"result_ok": 0, "gemm_ok": 0})
     budget = [n * len(stubs)]
     await asyncio.gather(*(client_loop(stub, pb, source, budget, out, trace) for stub in stubs))
     return out
@@ -395,13 +397,13 @@ def _loadgen_main(targets, first, source, concurrency, warmup, steps, barrier, r
         if go is not None:
             go.wait()
         t0 = time.perf_counter()
-        lat, errors, exec_times, phases = loop.run_until_complete(run_clients(stubs, source, steps))
-        results.put((time.perf_counter() - t0, lat, errors, exec_times, phases))
+        lat, errors, exec_times, phases, checks = loop.run_until_complete(run_clients(stubs, source, steps))
+        results.put((time.perf_counter() - t0, lat, errors, exec_times, phases, checks))
     except BaseException as e:  # noqa: BLE001 - report instead of hanging the barrier
         barrier.abort()
         if go is not None:
             go.abort()
-        results.put((0.0, [], [f"loadgen failed: {e!r}"[:300]], [], {}))
+        results.put((0.0, [], [f"loadgen failed: {e!r}"[:300]], [], {}, {}))
     finally:
         if chans:
             loop.run_until_complete(close_clients(chans))
@@ -668,18 +670,19 @@ def main():
             roles0 = cpu_by_role(svc_pid)
             trace = [] if os.environ.get("BEE_BENCH_TRACE") else None
             t0 = time.perf_counter()
-            lat, errors, exec_times, phases = loop.run_until_complete(run_clients(stubs, source, args.steps, trace))
+            lat, errors, exec_times, phases, checks = loop.run_until_complete(
+                run_clients(stubs, source, args.steps, trace))
             barrier()
             elapsed = time.perf_counter() - t0
             roles1 = cpu_by_role(svc_pid)
             cpu_busy = (cpu_usage_s()[0] - cpu0) / elapsed if elapsed > 0 else 0.0
-            gathered = [(elapsed, lat, errors, exec_times, phases)]
+            gathered = [(elapsed, lat, errors, exec_times, phases, checks)]
             if trace is not None:  # completion time (s after t0) and latency of every timed Execute
                 with open(os.environ["BEE_BENCH_TRACE"], "w") as fh:
                     json.dump([(round(t - t0, 6), l) for t, l in trace], fh)
             if world > 1:
                 gathered = [None] * world
-                dist.all_gather_object(gathered, (elapsed, lat, errors, exec_times, phases))
+                dist.all_gather_object(gathered, (elapsed, lat, errors, exec_times, phases, checks))
 
         # secondary: the same payload with every draw materialised in HBM
         # (the reference's numpy data movement), same clients, untimed by
@@ -765,7 +768,12 @@ def main():
             if all_err:
                 out["first_error"] = all_err[0][:400]
             out["per_gpu_rps"] = round(out["value"] / max(n_gpus, 1), 3)
-            out["gemm_verified"] = args.workload == "numpy_gpu" and not args.payload
+            # counted from the responses: every timed Execute's Result within
+            # 6 sigma and every row of its GEMM checked (result_ok / gemm_row_ok)
+            n_res = sum(g[5].get("result_ok", 0) for g in gathered)
+            n_gemm = sum(g[5].get("gemm_ok", 0) for g in gathered)
+            out["checked"] = {"result_ok": n_res, "gemm_rows_ok": n_gemm, "of": total}
+            out["gemm_verified"] = total > 0 and n_gemm == total
             if mat is not None:
                 out["materialized"] = mat
             if gang is not None:

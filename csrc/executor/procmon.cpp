@@ -4,6 +4,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <signal.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <cstdio>
@@ -143,6 +144,54 @@ int64_t vram_bytes(pid_t pid, std::set<std::string>* clients, bool* has_render) 
   return total;
 }
 
+namespace {
+
+pid_t parent_of(pid_t pid) {
+  char path[64], buf[1024];
+  snprintf(path, sizeof path, "/proc/%d/stat", (int)pid);
+  if (read_small(path, buf, sizeof buf) <= 0) return -1;
+  const char* rp = strrchr(buf, ')');
+  int ppid = -1;
+  if (!rp || sscanf(rp + 1, " %*c %d", &ppid) != 1) return -1;
+  return (pid_t)ppid;
+}
+
+// Signal `child`, read earlier from `parent`'s children list, only if it is
+// still that process: between the read and the signal the child may have
+// been reaped and its PID handed to an unrelated process (the daemon is
+// privileged enough to signal it).  A pidfd pins the process it was opened
+// on; its parent is checked after the open, so a recycled PID (whose parent
+// is someone else) is skipped, and a pinned process that dies before the
+// signal only makes the signal fail.
+bool signal_child(pid_t parent, pid_t child, int sig) {
+  const int fd = (int)syscall(SYS_pidfd_open, child, 0);
+  if (fd < 0) {
+    if (errno != ENOSYS) return false;  // gone already (ESRCH)
+    // kernels before pidfd (5.3): best effort, checked the same way
+    return parent_of(child) == parent && kill(child, sig) == 0;
+  }
+  bool ok = parent_of(child) == parent && syscall(SYS_pidfd_send_signal, fd, sig, nullptr, 0) == 0;
+  close(fd);
+  return ok;
+}
+
+// (parent, child) pairs of the tree below `leader`, breadth first
+void tree_edges(pid_t leader, std::vector<std::pair<pid_t, pid_t>>* out, size_t cap = 4096) {
+  out->clear();
+  std::vector<pid_t> frontier{leader}, kids;
+  for (size_t i = 0; i < frontier.size() && out->size() < cap; ++i) {
+    kids.clear();
+    children_of(frontier[i], &kids);
+    for (pid_t k : kids) {
+      if (out->size() >= cap) break;
+      out->emplace_back(frontier[i], k);
+      frontier.push_back(k);
+    }
+  }
+}
+
+}  // namespace
+
 int kill_tree(pid_t leader, int rounds) {
   if (leader <= 0) return 0;
   // freeze the leader's process group first (atomic for its members: a fork
@@ -151,14 +200,16 @@ int kill_tree(pid_t leader, int rounds) {
   kill(-leader, SIGSTOP);
   kill(leader, SIGSTOP);
   std::set<pid_t> signalled;
-  std::vector<pid_t> pids;
+  std::vector<std::pair<pid_t, pid_t>> edges;
   for (int r = 0; r < rounds; ++r) {
-    tree(leader, &pids);
+    tree_edges(leader, &edges);
     size_t fresh = 0;
-    for (pid_t p : pids) {
-      if (p == leader || !signalled.insert(p).second) continue;  // (killed ones linger as zombies)
-      kill(p, SIGKILL);
-      ++fresh;
+    for (auto& e : edges) {
+      if (e.second == leader || signalled.count(e.second)) continue;  // (killed ones linger as zombies)
+      if (signal_child(e.first, e.second, SIGKILL)) {
+        signalled.insert(e.second);
+        ++fresh;
+      }
     }
     if (!fresh) break;
   }
@@ -170,9 +221,10 @@ int kill_tree(pid_t leader, int rounds) {
 void signal_tree(pid_t leader, int sig) {
   if (leader <= 0) return;
   kill(-leader, sig);
-  std::vector<pid_t> pids;
-  tree(leader, &pids);
-  for (pid_t p : pids) kill(p, sig);
+  kill(leader, sig);
+  std::vector<std::pair<pid_t, pid_t>> edges;
+  tree_edges(leader, &edges);
+  for (auto& e : edges) signal_child(e.first, e.second, sig);
 }
 
 }  // namespace procmon

@@ -54,8 +54,9 @@ __device__ __forceinline__ C binary(C a, C b) {
   else if constexpr (OP == kBinSub) return a - b;
   else if constexpr (OP == kBinMul) return a * b;
   else if constexpr (OP == kBinDiv) return a / b;
-  else if constexpr (OP == kBinMax) return a > b ? a : b;
-  else if constexpr (OP == kBinMin) return a < b ? a : b;
+  // numpy.maximum / minimum: NaN in either operand gives NaN
+  else if constexpr (OP == kBinMax) return (a > b || a != a) ? a : b;
+  else if constexpr (OP == kBinMin) return (a < b || a != a) ? a : b;
   else return pow(a, b);
 }
 

@@ -15,6 +15,14 @@
 #include "bk_common.hpp"
 #include "bk_philox.hpp"
 
+// The completion-ticket fold below relies on GFX9-family memory semantics:
+// vmcnt counts stores and sc1 (agent-scope) accesses are coherent across
+// XCDs.  gfx10+ counts stores in vscnt, so the fold could read partials that
+// have not landed -- refuse to build for anything but gfx9 (gfx950 here).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "reduce.hip: the single-pass ticket fold is written for GFX9-family (gfx950) memory semantics"
+#endif
+
 namespace bk {
 
 // kRedMaxAbsDiff: max |a - b| (two operands, like kRedDot) -- one pass where
@@ -59,9 +67,12 @@ template <int OP> __device__ __forceinline__ double red_map(double a, double b) 
   else if constexpr (OP == kRedMaxAbsDiff) return fabs(a - b);
   else return a;
 }
+// max / min propagate NaN as numpy's max() / min() do (fmax / fmin are IEEE
+// maxNum: they drop a NaN operand, so a max-abs-difference check of a result
+// holding NaN would return a finite "error")
 template <int OP> __device__ __forceinline__ double red_combine(double x, double y) {
-  if constexpr (OP == kRedMax || OP == kRedMaxAbsDiff) return fmax(x, y);
-  else if constexpr (OP == kRedMin) return fmin(x, y);
+  if constexpr (OP == kRedMax || OP == kRedMaxAbsDiff) return (x != x || y != y) ? __builtin_nan("") : fmax(x, y);
+  else if constexpr (OP == kRedMin) return (x != x || y != y) ? __builtin_nan("") : fmin(x, y);
   else return x + y;
 }
 

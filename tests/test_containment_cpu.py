@@ -279,9 +279,14 @@ def test_cgroup_leaf_per_sandbox(tmp_path):
                 for leaf in root.iterdir():
                     if leaf.is_dir() and leaf.name.startswith("bee-") and (leaf / "cgroup.procs").exists():
                         try:
-                            seen[leaf.name] = {f.name: f.read_text() for f in leaf.iterdir()}
+                            snap = {f.name: f.read_text() for f in leaf.iterdir()}
                         except OSError:
-                            pass
+                            continue
+                        # keep the last snapshot taken while the sandbox was
+                        # in it (a read racing the leaf's set-up or teardown
+                        # must not replace it)
+                        if snap.get("cgroup.procs", "").strip():
+                            seen[leaf.name] = snap
                 time.sleep(0.01)
 
         t = threading.Thread(target=watch)

@@ -70,3 +70,28 @@ def test_single_gpu_requests_spread_and_gang_after(two_slot_service):
     assert {g for r in rs for g in r.gpu_ids} == {0, 1}
     r = h.call(h.ctx.code_executor.execute(source_code=GANG_GLOO, gpus=2, nprocs=2, timeout=120), timeout=300)
     assert r.exit_code == 0 and r.stdout.count("sum=3.0") == 2, (r.stdout, r.stderr)
+
+
+GANG_REINIT = textwrap.dedent(
+    """
+    import os, torch, torch.distributed as dist
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    for round_ in range(3):  # init -> destroy -> init: a fresh FileStore file each time
+        dist.init_process_group("gloo")
+        x = torch.tensor([float(rank + 1 + round_)])
+        dist.all_reduce(x)
+        print(f"round{round_} rank{rank} sum={x.item()}")
+        dist.destroy_process_group()
+    """
+)
+
+
+def test_gang_reinitialises_process_group(two_slot_service):
+    """The default (FileStore) rendezvous survives init / destroy / init in
+    one job: each init takes a fresh file (sandbox_patches.next_rendezvous),
+    where re-using the first group's file could hang or fail."""
+    h = two_slot_service
+    r = h.call(h.ctx.code_executor.execute(source_code=GANG_REINIT, gpus=2, nprocs=2, timeout=120), timeout=300)
+    assert r.exit_code == 0, r.stderr
+    for k in range(3):
+        assert r.stdout.count(f"round{k} ") == 2 and f"sum={3.0 + 2 * k}" in r.stdout, r.stdout

@@ -701,6 +701,28 @@ def test_max_abs_diff(gpu, dtype, n):
     assert float(gpu.max_abs_diff(a, b)) == pytest.approx(want, rel=1e-6)
 
 
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+@pytest.mark.parametrize("n", [1, 4096, 1_000_003])
+@pytest.mark.parametrize("where", ["first", "middle", "last"])
+def test_max_min_propagate_nan_like_numpy(gpu, dtype, n, where):
+    """One NaN anywhere (any block, the fold's first or last partial) makes
+    max / min / max_abs_diff NaN, as numpy's max() does: a check of a result
+    against its reference must not read a corrupt result as a small error."""
+    rng = np.random.default_rng(n)
+    h = rng.standard_normal(n)
+    h[{"first": 0, "middle": n // 2, "last": n - 1}[where]] = np.nan
+    x = gpu.asarray(h, dtype)
+    y = gpu.asarray(np.zeros(n), dtype)
+    assert np.isnan(np.abs(h).max())  # numpy's answer
+    assert np.isnan(float(gpu.amax(x))) and np.isnan(float(gpu.amin(x)))
+    assert np.isnan(float(gpu.max_abs_diff(x, y))) and np.isnan(float(gpu.max_abs_diff(y, x)))
+    # elementwise maximum / minimum: NaN in either operand
+    m = gpu.maximum(y, x).numpy()
+    assert np.array_equal(np.isnan(m), np.isnan(np.maximum(np.zeros(n), h)))
+    m = gpu.minimum(x, y).numpy()
+    assert np.array_equal(np.isnan(m), np.isnan(np.minimum(h, np.zeros(n))))
+
+
 SEGMENT_PROBE = r"""
 import ctypes, random
 import numpy as np

@@ -561,6 +561,10 @@ def test_precompiled_payload_roundtrip():
 
     assert set(names(code)) == {"/workspace/main.py"}
     assert precompiled("print(\n") is None  # the sandbox reports the SyntaxError itself
+    # a compile that warns stays in the sandbox (its stderr shows the warning
+    # on every run, not the front-end's on the repeated ones)
+    assert precompiled("x = 1\nassert (x, 'always true')\n") is None
+    assert precompiled("x = 1\nprint(x is 1)\n") is None
     assert load_precompiled(precompiled("echo hi\n"), "/x.py")[1] is True  # xonsh-lowered
     assert load_precompiled("not base64 !", "/x.py") is None
     assert load_precompiled(__import__("base64").b64encode(b"\0\0\0\0P...").decode(), "/x.py") is None
