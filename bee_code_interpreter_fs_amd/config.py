@@ -221,6 +221,11 @@ class Config:
     # ("" = the executor's own cgroup)
     sandbox_cgroup: str = "auto"
     sandbox_cgroup_root: str = ""
+    # numpy offload for every request (a request's numpy_offload field
+    # overrides it): numpy.random draws of >= 2**20 elements live on the
+    # sandbox's GPU and numpy functions on them run on the beekern kernels
+    # (ops/numpy_offload.py); off = numpy semantics and placement unchanged
+    numpy_offload: bool = False
 
     def __init__(self, _env: Optional[Mapping[str, str]] = None, **overrides: Any) -> None:
         env = os.environ if _env is None else _env

@@ -51,6 +51,8 @@ CODE_INTERPRETER_FIELDS = {
         Field("gpus", 101, INT32),
         Field("hbm_bytes", 102, INT64),
         Field("source_file", 103, STRING),
+        # unset = the service default (APP_NUMPY_OFFLOAD); ops/numpy_offload.py
+        Field("numpy_offload", 104, BOOL, proto3_optional=True),
     ],
     "ExecuteResponse": [
         Field("stdout", 1, STRING),

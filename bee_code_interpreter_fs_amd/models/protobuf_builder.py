@@ -47,6 +47,10 @@ class Field:
     type: Union[str, Map]  # scalar name, ".pkg.Message", "enum:.pkg.Enum" or Map
     repeated: bool = False
     oneof: Optional[str] = None
+    # proto3 `optional`: presence is tracked (HasField), so "unset" differs
+    # from the zero value (a synthetic one-field oneof, declared after the
+    # real ones as protoc does)
+    proto3_optional: bool = False
 
 
 @dataclass
@@ -91,6 +95,7 @@ def build_file(
             for vname, vnum in values:
                 ep.value.add(name=vname, number=vnum)
         oneofs: List[str] = []
+        optional: List = []
         for f in msg.fields:
             fp = mp.field.add(name=f.name, number=f.number, json_name=_lower_camel(f.name))
             if isinstance(f.type, Map):
@@ -110,6 +115,12 @@ def build_file(
                     oneofs.append(f.oneof)
                     mp.oneof_decl.add(name=f.oneof)
                 fp.oneof_index = oneofs.index(f.oneof)
+            elif f.proto3_optional:
+                optional.append(fp)
+        for fp in optional:
+            mp.oneof_decl.add(name="_" + fp.name)
+            fp.oneof_index = len(mp.oneof_decl) - 1
+            fp.proto3_optional = True
     for svc in services:
         sp = fdp.service.add(name=svc.name)
         for m in svc.methods:

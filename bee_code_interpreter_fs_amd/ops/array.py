@@ -208,6 +208,19 @@ class DeviceArray:
         a = self.numpy()
         return a.astype(dtype) if dtype is not None else a
 
+    # numpy functions and ufuncs on a device array run on the kernels where
+    # one computes what numpy would; the rest copy to the host once, with a
+    # warning (ops/npinterop.py) -- not silently through __array__
+    def __array_ufunc__(self, ufunc, method, *inputs, **kwargs):
+        from .npinterop import array_ufunc
+
+        return array_ufunc(_binding(), ufunc, method, inputs, kwargs)
+
+    def __array_function__(self, func, types, args, kwargs):
+        from .npinterop import array_function
+
+        return array_function(_binding(), func, types, args, kwargs)
+
     def tolist(self):
         return self.numpy().tolist()
 
@@ -280,6 +293,22 @@ class DeviceArray:
     def __neg__(self): return _unary("negative", self)
     def __abs__(self): return _unary("abs", self)
     def __matmul__(self, o): return matmul(self, o)
+
+
+_BINDING = []
+
+
+def _binding():
+    """DeviceArray's plug into the numpy protocols (ops/npinterop.py)."""
+    if not _BINDING:
+        from .npinterop import Binding
+
+        def mine(x):
+            return isinstance(x, DeviceArray)
+
+        _BINDING.append(Binding(dev=lambda x: x if mine(x) else None, box=lambda d: d,
+                                host=lambda x: x.numpy(), is_mine=mine))
+    return _BINDING[0]
 
 
 def _np_dtype(dtype: str):

@@ -191,6 +191,18 @@ class _PatchFinder(importlib.abc.MetaPathFinder):
 _INSTALLED = False
 
 
+def add_patch(name: str, patch: Callable) -> None:
+    """A per-run patch (e.g. the numpy offload, ops/numpy_offload.py):
+    applied now if ``name`` is imported already, else when it is."""
+    mod = sys.modules.get(name)
+    if mod is not None:
+        patch(mod)
+        return
+    PATCHES[name] = patch
+    if not any(isinstance(f, _PatchFinder) for f in sys.meta_path):
+        sys.meta_path.insert(0, _PatchFinder())
+
+
 def install() -> None:
     """Idempotent: the zygote installs the patches once before forking, so a
     worker's call is free (modules imported later go through the finder)."""

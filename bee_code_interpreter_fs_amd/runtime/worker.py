@@ -319,6 +319,7 @@ _KEEP: list = []
 
 
 _PATHS_FOR: list = []  # the runtime-packages view _prepare_paths ran for
+_NUMPY_OFFLOAD: list = []  # non-empty: this run asked for the numpy offload
 
 
 def _prepare_paths(runtime_packages: str) -> None:
@@ -344,6 +345,12 @@ def run_script(script: str, argv, workspace: str, runtime_packages: str, precomp
     from . import sandbox_patches
 
     sandbox_patches.install()
+    if _NUMPY_OFFLOAD:
+        # large numpy.random draws live on the GPU and numpy calls on them
+        # dispatch to the kernels (ops/numpy_offload.py)
+        from bee_code_interpreter_fs_amd.ops import numpy_offload
+
+        numpy_offload.install()
     lowered = None
     pre = load_precompiled(precompiled, script) if precompiled else None
     try:
@@ -683,6 +690,8 @@ def _serve(cwd: str, chan: _Chan) -> None:
         job_env = job.get("env") or {}
         for k, v in job_env.items():
             os.environ[k] = str(v)
+        if job.get("numpy_offload") or os.environ.get("BEE_NUMPY_OFFLOAD") == "1":
+            _NUMPY_OFFLOAD.append(True)
         _apply_job_quota(int(job.get("hbm_quota") or 0))
         if _REDIRECTED != [job["stdout"], job["stderr"]]:
             _redirect_stdio(job["stdout"], job["stderr"])

@@ -38,6 +38,9 @@ class ExecuteRequest:
     hbm_bytes: Optional[int] = None  # per-request HBM quota override
     nprocs: int = 1  # >1: launch one rank per GPU with torch.distributed env
     env: Mapping[str, str] = field(default_factory=dict)
+    # numpy.random draws + numpy calls on them on the GPU (ops/numpy_offload.py);
+    # None = the service default (APP_NUMPY_OFFLOAD)
+    numpy_offload: Optional[bool] = None
 
     def validate(self) -> "ExecuteRequest":
         if (self.source_code is None) == (self.source_file is None):
@@ -81,6 +84,7 @@ class CodeExecutor(abc.ABC):
         hbm_bytes: Optional[int] = None,
         nprocs: int = 1,
         env: Optional[Mapping[str, str]] = None,
+        numpy_offload: Optional[bool] = None,
     ) -> ExecutionResult:
         req = ExecuteRequest(
             source_code=source_code,
@@ -91,6 +95,7 @@ class CodeExecutor(abc.ABC):
             hbm_bytes=hbm_bytes,
             nprocs=nprocs,
             env=dict(env or {}),
+            numpy_offload=numpy_offload,
         ).validate()
         return await self.run(req)
 

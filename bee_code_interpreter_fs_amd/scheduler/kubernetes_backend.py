@@ -201,6 +201,8 @@ class KubernetesBackend(CodeExecutor):
 
             await asyncio.gather(*(upload(p, o) for p, o in request.files.items()))
             body = {"timeout": timeout}
+            if request.numpy_offload:
+                body["numpy_offload"] = True  # the pod's executor hands it to the sandbox
             if request.source_file is not None:
                 body["source_file"] = request.source_file
             else:

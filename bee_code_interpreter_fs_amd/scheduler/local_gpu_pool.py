@@ -423,6 +423,9 @@ class LocalGpuPoolBackend(CodeExecutor):
                 body["gpus"] = ""  # CPU-only sandbox on a GPU slot
             if request.env:
                 body["env"] = dict(request.env)
+            offload = self.config.numpy_offload if request.numpy_offload is None else request.numpy_offload
+            if offload and want > 0:
+                body["numpy_offload"] = True  # a job field: the pooled sandbox applies it (ops/numpy_offload.py)
             try:
                 resp = await lead.executor.post("/v1/execute", body, timeout=body["timeout"] + 180.0)
             except (UdsHttpError, OSError, AssertionError) as e:

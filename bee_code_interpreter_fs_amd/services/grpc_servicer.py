@@ -83,6 +83,8 @@ class CodeInterpreterServicer:
                 kwargs["nprocs"] = request.gpus
         if request.hbm_bytes > 0:
             kwargs["hbm_bytes"] = request.hbm_bytes
+        if request.HasField("numpy_offload"):
+            kwargs["numpy_offload"] = request.numpy_offload
         try:
             result = await self.code_executor.execute(**kwargs)
         except FileNotFoundError as e:

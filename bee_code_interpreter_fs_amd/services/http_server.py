@@ -51,6 +51,7 @@ class ExecuteRequest(BaseModel):
     gpus: Optional[int] = Field(default=None, ge=0, le=64)
     hbm_bytes: Optional[int] = Field(default=None, ge=0)
     nprocs: int = Field(default=1, ge=1, le=64)
+    numpy_offload: Optional[bool] = None  # None = APP_NUMPY_OFFLOAD (ops/numpy_offload.py)
 
 
 class ExecuteResponse(BaseModel):
@@ -170,6 +171,8 @@ def create_http_server(code_executor, custom_tool_executor: CustomToolExecutor, 
         if request.gpus is not None:
             kwargs["gpus"] = request.gpus
             kwargs["nprocs"] = request.nprocs
+        if request.numpy_offload is not None:
+            kwargs["numpy_offload"] = request.numpy_offload
         if request.source_file is not None:
             kwargs["source_file"] = request.source_file
         else:

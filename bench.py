@@ -75,7 +75,9 @@ WORKLOADS = {
         "float64 (rand/square/sum) + bf16 (GEMM)",
     ),
     "numpy_cpu": (
-        "examples/benchmark_numpy_cpu.py",
+        # the reference's payload verbatim; --numpy-offload runs it on the GPU
+        # (ops/numpy_offload.py), without it numpy runs on the CPU
+        "examples/benchmark_numpy_reference.py",
         "Execute RPCs/sec (unmodified benchmark-numpy payload, numpy on CPU)",
         "benchmark-numpy.py payload: 1e8 f64 numpy rand+square+sum per Execute",
         "float64",
@@ -127,6 +129,9 @@ def parse_args():
     p.add_argument("--no-gang-check", action="store_true")
     p.add_argument("--max-inflight", type=int, default=0,
                    help="admitted executions per GPU (each daemon's bound for all front-ends; 0 = 2 x concurrency)")
+    p.add_argument("--numpy-offload", action="store_true",
+                   help="Execute with numpy_offload=True: numpy.random draws of the payload live on the sandbox's GPU "
+                        "and numpy calls on them run on the beekern kernels (ops/numpy_offload.py)")
     p.add_argument("--materialized-steps", type=int, default=-1,
                    help="steps of the secondary materialised-draw run (numpy's HBM traffic; -1 = min(steps, 20), 0 = skip)")
     return p.parse_args()
@@ -332,13 +337,13 @@ async def close_clients(chans):
     await asyncio.gather(*(c.close() for c in chans), return_exceptions=True)
 
 
-async def client_loop(stub, pb, source, budget, out, trace=None):
+async def client_loop(stub, pb, source, budget, out, trace=None, extra=None):
     lat, errors, exec_times, phases, checks = out
     while budget[0] > 0:
         budget[0] -= 1  # (one event loop: taken before the await, no race)
         t = time.perf_counter()
         try:
-            r = await stub.Execute(pb.ExecuteRequest(source_code=source), timeout=600)
+            r = await stub.Execute(pb.ExecuteRequest(source_code=source, **(extra or {})), timeout=600)
         except Exception as e:  # noqa: BLE001
             errors.append(repr(e)[:300])
             continue
@@ -365,7 +370,7 @@ async def client_loop(stub, pb, source, budget, out, trace=None):
             errors.append(f"exit={r.exit_code} stdout={r.stdout[-200:]!r} stderr={r.stderr[-500:]!r}")
 
 
-async def run_clients(stubs, source, n, trace=None):
+async def run_clients(stubs, source, n, trace=None, extra=None):
     """``n`` steps of ``len(stubs)`` closed-loop clients: ``n * len(stubs)``
     Executes, each client taking the next one from the shared budget as soon
     as its previous one returns (``hey -n N -c C`` style).  With a fixed
@@ -377,11 +382,11 @@ async def run_clients(stubs, source, n, trace=None):
 
     out = ([], [], [], {}, {"result_ok": 0, "gemm_ok": 0})
     budget = [n * len(stubs)]
-    await asyncio.gather(*(client_loop(stub, pb, source, budget, out, trace) for stub in stubs))
+    await asyncio.gather(*(client_loop(stub, pb, source, budget, out, trace, extra) for stub in stubs))
     return out
 
 
-def _loadgen_main(targets, first, source, concurrency, warmup, steps, barrier, results, go=None):
+def _loadgen_main(targets, first, source, concurrency, warmup, steps, barrier, results, go=None, extra=None):
     """One load-generator process (single-process ``--gpus N`` runs start N
     of them, so offered load grows with N like the torchrun ranks do).
     ``barrier``: every load generator of this process tree has warmed up;
@@ -392,12 +397,13 @@ def _loadgen_main(targets, first, source, concurrency, warmup, steps, barrier, r
     chans = []
     try:
         chans, stubs = loop.run_until_complete(open_clients(targets, first, concurrency))
-        loop.run_until_complete(run_clients(stubs, source, warmup))
+        loop.run_until_complete(run_clients(stubs, source, warmup, extra=extra))
         barrier.wait()
         if go is not None:
             go.wait()
         t0 = time.perf_counter()
-        lat, errors, exec_times, phases, checks = loop.run_until_complete(run_clients(stubs, source, steps))
+        lat, errors, exec_times, phases, checks = loop.run_until_complete(run_clients(stubs, source, steps,
+                                                                                     extra=extra))
         results.put((time.perf_counter() - t0, lat, errors, exec_times, phases, checks))
     except BaseException as e:  # noqa: BLE001 - report instead of hanging the barrier
         barrier.abort()
@@ -410,7 +416,7 @@ def _loadgen_main(targets, first, source, concurrency, warmup, steps, barrier, r
         loop.close()
 
 
-def run_loadgens(n_procs, targets, source, concurrency, warmup, steps, sync, marks=None, first=0):
+def run_loadgens(n_procs, targets, source, concurrency, warmup, steps, sync, marks=None, first=0, extra=None):
     """``n_procs`` client processes of ``concurrency`` clients each; times
     the steps between one barrier all of them (and this process) pass and
     their completion.  Returns the gathered tuples (elapsed per process)."""
@@ -420,7 +426,7 @@ def run_loadgens(n_procs, targets, source, concurrency, warmup, steps, sync, mar
     barrier, go = ctx.Barrier(n_procs + 1), ctx.Barrier(n_procs + 1)
     results = ctx.Queue()
     procs = [ctx.Process(target=_loadgen_main, args=(targets, first + i * concurrency, source, concurrency, warmup,
-                                                     steps, barrier, results, go), daemon=True)
+                                                     steps, barrier, results, go, extra), daemon=True)
              for i in range(n_procs)]
     for p in procs:
         p.start()
@@ -616,6 +622,9 @@ def main():
 
     script, metric, model, dtype = WORKLOADS[args.workload]
     source = open(args.payload or os.path.join(ROOT, script)).read()
+    extra = {"numpy_offload": True} if args.numpy_offload else None
+    if args.numpy_offload:
+        metric = metric.replace("numpy on CPU", "numpy offloaded to the GPU (numpy_offload)")
     loop = asyncio.new_event_loop()
     proc = None
     tmp = tempfile.mkdtemp(prefix="bee-bench-", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
@@ -658,20 +667,20 @@ def main():
         if loadgens > 1:
             marks = {"roles0": None, "svc": svc_pid}
             gathered = gather_ranks(run_loadgens(loadgens, targets, source, per_lg, args.warmup, args.steps, barrier,
-                                                 marks, first=first))
+                                                 marks, first=first, extra=extra))
             elapsed = max(g[0] for g in gathered)
             cpu_busy = (cpu_usage_s()[0] - marks["cpu0"]) / max(time.perf_counter() - marks["t0"], 1e-9)
             roles0, roles1 = marks["roles0"], marks.get("roles1")
         else:
             chans, stubs = loop.run_until_complete(open_clients(targets, first, args.concurrency))
-            loop.run_until_complete(run_clients(stubs, source, args.warmup))  # warm every pool
+            loop.run_until_complete(run_clients(stubs, source, args.warmup, extra=extra))  # warm every pool
             barrier()
             cpu0, cpu_src = cpu_usage_s()
             roles0 = cpu_by_role(svc_pid)
             trace = [] if os.environ.get("BEE_BENCH_TRACE") else None
             t0 = time.perf_counter()
             lat, errors, exec_times, phases, checks = loop.run_until_complete(
-                run_clients(stubs, source, args.steps, trace))
+                run_clients(stubs, source, args.steps, trace, extra=extra))
             barrier()
             elapsed = time.perf_counter() - t0
             roles1 = cpu_by_role(svc_pid)
@@ -768,6 +777,8 @@ def main():
             if all_err:
                 out["first_error"] = all_err[0][:400]
             out["per_gpu_rps"] = round(out["value"] / max(n_gpus, 1), 3)
+            if args.numpy_offload:
+                out["numpy_offload"] = True  # the payload is unmodified numpy; its draws and reductions ran on the GPU
             # counted from the responses: every timed Execute's Result within
             # 6 sigma and every row of its GEMM checked (result_ok / gemm_row_ok)
             n_res = sum(g[5].get("result_ok", 0) for g in gathered)

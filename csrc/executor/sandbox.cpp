@@ -1349,6 +1349,7 @@ SandboxPool::RunResult SandboxPool::run_in(const std::shared_ptr<Worker>& w, con
   msg.set("hbm_quota", (int64_t)spec.hbm_quota);
   msg.set("env", spec.env);
   if (!spec.code.empty()) msg.set("code", spec.code);
+  if (spec.numpy_offload) msg.set("numpy_offload", true);
   int fd;
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -1625,6 +1626,7 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   // a source_code payload the front-end compiled: handed to the sandbox as is
   // (the sandbox only trusts it as far as its own code: it runs it itself)
   if (has_code && req["code"].is_string()) spec.code = req["code"].as_string();
+  spec.numpy_offload = req["numpy_offload"].as_bool();
   {
     std::lock_guard<std::mutex> lk(mu_);
     for (auto& w : ranks) w->set_quota(spec.hbm_quota);  // the broker charges against this

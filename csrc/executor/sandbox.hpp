@@ -270,6 +270,7 @@ class SandboxPool {
     int64_t hbm_quota = 0;
     Json env = Json::object();
     std::string code;  // the front-end's precompiled payload (opaque to the daemon), "" = none
+    bool numpy_offload = false;  // the sandbox routes large numpy.random draws to the GPU (ops/numpy_offload.py)
   };
   struct RunResult {
     std::string stdout_text, stderr_text;
