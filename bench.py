@@ -28,6 +28,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
+import math
 import os
 import socket
 import statistics
@@ -127,6 +128,9 @@ def parse_args():
                    help="CPU rehearsal of an N-GPU node: N executors pinned to GPU ids 0..N-1 that need not exist "
                         "(no kernel broker, no HIP warm-up); use with a CPU workload such as --workload hello")
     p.add_argument("--no-gang-check", action="store_true")
+    p.add_argument("--fold", action="store_true",
+                   help="keep one executor daemon (broker, HIP context, pools) per requested GPU even when fewer GPUs "
+                        "are visible: the N-GPU node's topology rehearsed on this box")
     p.add_argument("--max-inflight", type=int, default=0,
                    help="admitted executions per GPU (each daemon's bound for all front-ends; 0 = 2 x concurrency)")
     p.add_argument("--numpy-offload", action="store_true",
@@ -239,10 +243,80 @@ def free_port() -> int:
 
 def gpu_ids(n_gpus: int, args):
     """One executor per GPU; a run with more ranks than visible GPUs folds the
-    extra ranks onto the existing devices (and says so in the JSON)."""
+    extra ranks onto the existing devices (and says so in the JSON).  With
+    --fold, every rank keeps an executor daemon of its own -- N daemons,
+    brokers and HIP contexts -- on the visible GPUs: the N-GPU node's process
+    topology rehearsed on fewer GPUs."""
     if args.virtual_gpus:
         return list(range(n_gpus))
+    if args.fold:
+        return [i % visible_gpus() for i in range(n_gpus)]
     return sorted({i % visible_gpus() for i in range(n_gpus)})
+
+
+def cpu_quota_cores() -> tuple:
+    """(CPUs of time this job may use per period, source): the cgroup CPU
+    quota (scheduler/topology.py cpu_quota), else the CPUs it may run on."""
+    from bee_code_interpreter_fs_amd.scheduler.topology import cpu_quota
+
+    q = cpu_quota()
+    if q > 0:
+        return q, "cgroup cpu.max"
+    try:
+        return float(len(os.sched_getaffinity(0))), "affinity"
+    except (AttributeError, OSError):
+        return float(os.cpu_count() or 1), "cpu_count"
+
+
+def frontends_for(n_slots: int, quota: float) -> int:
+    """Front-end replicas: three per GPU slot (measured on one GPU: a
+    replica saturates a core at ~2.2k Execute/s, and a third one per GPU
+    took p50 down, profiles/archive/r2_s3_frontends3_ab.log), but no more
+    than one per ~5 cores of the CPU quota -- at ~4.5 ms of CPU per Execute a
+    5-core share carries ~1.1k Execute/s, half a replica's capacity; 24
+    replicas on a 16-core quota (8 slots folded onto one GPU box) would only
+    add processes that compete with the sandboxes for the same quota."""
+    per_gpu = 3 * max(1, n_slots)
+    return max(min(3, per_gpu), min(per_gpu, int(math.ceil(quota / 5.0))), 1)
+
+
+def pss_by_role(service_pid):
+    """Proportional set size (MB) of the service's processes by role: a
+    shared page counts once across the node (smaps_rollup Pss)."""
+    roles = {"frontend": 0.0, "executor_daemon": 0.0, "zygote": 0.0, "pooled_sandboxes": 0.0}
+    if service_pid is None:
+        return roles
+    stack, seen = [(service_pid, None)], set()
+    while stack:
+        pid, parent_role = stack.pop()
+        if pid in seen:
+            continue
+        seen.add(pid)
+        try:
+            with open(f"/proc/{pid}/cmdline", "rb") as f:
+                cmd = f.read()
+            with open(f"/proc/{pid}/smaps_rollup") as f:
+                pss = next((int(l.split()[1]) for l in f if l.startswith("Pss:")), 0) / 1024.0
+        except (OSError, StopIteration, ValueError):
+            continue
+        role = ("pooled_sandboxes" if parent_role == "zygote" else "executor_daemon" if b"bee-executor" in cmd
+                else "zygote" if b"zygote" in cmd else "frontend")
+        roles[role] += pss
+        stack.extend((c, role) for c in _children(pid))
+    return {k: round(v, 1) for k, v in roles.items()}
+
+
+def slot_executions(hport):
+    """Executions so far of every GPU slot's daemon (for the per-slot
+    balance of the timed region)."""
+    import urllib.request
+
+    try:
+        with urllib.request.urlopen(f"http://127.0.0.1:{hport}/v1/status", timeout=10) as f:
+            st = json.load(f)
+        return [int(s["executor"].get("executions", 0)) for s in st["slots"]]
+    except Exception:  # noqa: BLE001
+        return None
 
 
 def start_service(tmp: str, n_gpus: int, args):
@@ -255,7 +329,8 @@ def start_service(tmp: str, n_gpus: int, args):
     # every N keeps each replica's share of the offered load (8 clients per
     # GPU) what it is on one GPU -- weak scaling of the front-end too (24 at
     # N = 8; front-ends hold no GPU context)
-    frontends = args.frontends or min(32, 3 * max(1, n_gpus))
+    frontends = args.frontends or frontends_for(len(gpu_ids(n_gpus, args)) if not args.cpu_only else 1,
+                                                cpu_quota_cores()[0])
     routed = None if args.payload else ROUTED_POOL[args.workload]
 
     def pool(kind: str) -> str:
@@ -290,6 +365,10 @@ def start_service(tmp: str, n_gpus: int, args):
             ),
         }
     )
+    if args.fold and len(set(gpu_ids(n_gpus, args))) < n_gpus:
+        # folded slots share the card: no warm direct (HIP-context) sandboxes,
+        # so the processes holding the GPU stay the slots' daemons (brokers)
+        env["APP_WORKERS_PER_GPU_TARGET"] = "0"
     if args.virtual_gpus:
         # a CPU rehearsal of the node's scheduling: lean pools (one zygote of
         # each kind per slot), no kernel broker, no HIP warm-up
@@ -442,6 +521,8 @@ def run_loadgens(n_procs, targets, source, concurrency, warmup, steps, sync, mar
     if marks is not None:
         marks["t0"], marks["cpu0"] = time.perf_counter(), cpu_usage_s()[0]
         marks["roles0"] = cpu_by_role(marks.get("svc"))
+        if marks.get("hport"):
+            marks["slots0"] = slot_executions(marks["hport"])
     out = [results.get(timeout=3600) for _ in procs]
     sync()
     for p in procs:
@@ -449,6 +530,8 @@ def run_loadgens(n_procs, targets, source, concurrency, warmup, steps, sync, mar
     if marks is not None:
         # (after the join: the load generators' CPU is then in our children's)
         marks["roles1"] = cpu_by_role(marks.get("svc"))
+        if marks.get("hport"):
+            marks["slots1"] = slot_executions(marks["hport"])
     return out
 
 
@@ -631,9 +714,11 @@ def main():
     info = [None, None, None, None]
     chans = []
     try:
+        t_start = time.perf_counter()
         if rank == 0:
             proc, gport, hport, frontends, replicas = start_service(tmp, n_gpus, args)
             info = [gport, hport, frontends, replicas]
+        ready_s = time.perf_counter() - t_start  # service start -> READY (pools warm, self-warm done)
         if world > 1:
             dist.broadcast_object_list(info, src=0)
         gport, hport, frontends, replicas = info
@@ -665,18 +750,20 @@ def main():
         cpu0, cpu_src = cpu_usage_s()
         svc_pid = proc.pid if proc is not None else None
         if loadgens > 1:
-            marks = {"roles0": None, "svc": svc_pid}
+            marks = {"roles0": None, "svc": svc_pid, "hport": hport if rank == 0 else None}
             gathered = gather_ranks(run_loadgens(loadgens, targets, source, per_lg, args.warmup, args.steps, barrier,
                                                  marks, first=first, extra=extra))
             elapsed = max(g[0] for g in gathered)
             cpu_busy = (cpu_usage_s()[0] - marks["cpu0"]) / max(time.perf_counter() - marks["t0"], 1e-9)
             roles0, roles1 = marks["roles0"], marks.get("roles1")
+            slots0, slots1 = marks.get("slots0"), marks.get("slots1")
         else:
             chans, stubs = loop.run_until_complete(open_clients(targets, first, args.concurrency))
             loop.run_until_complete(run_clients(stubs, source, args.warmup, extra=extra))  # warm every pool
             barrier()
             cpu0, cpu_src = cpu_usage_s()
             roles0 = cpu_by_role(svc_pid)
+            slots0 = slot_executions(hport) if rank == 0 else None
             trace = [] if os.environ.get("BEE_BENCH_TRACE") else None
             t0 = time.perf_counter()
             lat, errors, exec_times, phases, checks = loop.run_until_complete(
@@ -684,6 +771,7 @@ def main():
             barrier()
             elapsed = time.perf_counter() - t0
             roles1 = cpu_by_role(svc_pid)
+            slots1 = slot_executions(hport) if rank == 0 else None
             cpu_busy = (cpu_usage_s()[0] - cpu0) / elapsed if elapsed > 0 else 0.0
             gathered = [(elapsed, lat, errors, exec_times, phases, checks)]
             if trace is not None:  # completion time (s after t0) and latency of every timed Execute
@@ -732,15 +820,20 @@ def main():
             for g in gathered:
                 for k, v in g[4].items():
                     all_phases.setdefault(k, []).extend(v)
+            ids = gpu_ids(n_gpus, args)
+            # (a gang needs n distinct GPUs: RCCL refuses two ranks on one
+            # device, so a folded rehearsal skips it)
             gang = (
                 gang_allreduce_check(target, n_gpus)
-                if n_gpus > 1 and not args.no_gang_check and not args.cpu_only
+                if n_gpus > 1 and not args.no_gang_check and not args.cpu_only and len(set(ids)) >= n_gpus
                 else None
             )
             total = len(all_lat)
             clients = per_lg * loadgens * world
-            pods = 1 if args.cpu_only else len(gpu_ids(n_gpus, args))
+            pods = 1 if args.cpu_only else len(ids)
             kind = "CPU-only" if args.cpu_only else "virtual-GPU (CPU rehearsal)" if args.virtual_gpus else "GPU-pinned"
+            if not args.cpu_only and not args.virtual_gpus and len(set(ids)) < len(ids):
+                kind += f" (folded onto {len(set(ids))} physical GPU(s): one daemon, broker and HIP context per slot)"
             out = {
                 "metric": metric,
                 "value": round(total / max_elapsed, 3) if max_elapsed > 0 else 0.0,
@@ -799,6 +892,33 @@ def main():
                 per["all_cgroup"] = round(cpu_busy * max_elapsed * 1e3 / total, 3)
                 per["unattributed"] = round(per["all_cgroup"] - sum(v for k, v in per.items() if k != "all_cgroup"), 3)
                 out["cpu_ms_per_exec"] = per
+            out["ready_s"] = round(ready_s, 2)
+            # what bounds this node: the CPU quota over CPU per Execute is the
+            # rate the service could reach with the GPUs idle; a run near it is
+            # CPU-bound (more GPUs would not help), one well below it is set by
+            # latency / GPU time at the offered concurrency
+            quota, quota_src = cpu_quota_cores()
+            bound = {"cpu_quota_cores": round(quota, 2), "quota_source": quota_src,
+                     "cpu_utilisation_of_quota": round(cpu_busy / quota, 3) if quota else None}
+            if "cpu_ms_per_exec" in out and out["cpu_ms_per_exec"]["all_cgroup"] > 0:
+                cap = quota * 1e3 / out["cpu_ms_per_exec"]["all_cgroup"]
+                bound["cpu_bound_rps"] = round(cap, 1)
+                # the same without the load generators (they share this box's
+                # quota here; production clients run elsewhere)
+                svc_ms = out["cpu_ms_per_exec"]["all_cgroup"] - out["cpu_ms_per_exec"].get("bench_clients", 0.0)
+                if svc_ms > 0:
+                    bound["cpu_bound_rps_service_only"] = round(quota * 1e3 / svc_ms, 1)
+                bound["fraction_of_cpu_bound"] = round(out["value"] / cap, 3)
+                bound["bound_by"] = "cpu" if out["value"] >= 0.85 * cap or cpu_busy >= 0.9 * quota else \
+                    "latency/gpu at this concurrency"
+            out["node_bound"] = bound
+            out["pss_mb"] = pss_by_role(svc_pid)
+            if slots0 and slots1 and len(slots0) == len(slots1):
+                per_slot = [b - a for a, b in zip(slots0, slots1)]
+                mean = sum(per_slot) / len(per_slot)
+                out["slot_balance"] = {"executions": per_slot,
+                                       "max_dev_from_mean": round(max(abs(x - mean) for x in per_slot) / mean, 3)
+                                       if mean else None}
             print(json.dumps(out), flush=True)
         if world > 1:
             dist.barrier()
