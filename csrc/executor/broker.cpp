@@ -71,7 +71,10 @@ class HipDevice final : public broker::Device {
   // straight into pinned host-coherent memory, so a reduce costs one stream
   // sync instead of a staging copy plus the sync.
   struct Ctx {
-    hipStream_t s = nullptr;
+    hipStream_t s = nullptr;   // the stream the session's latest op went to (waits and frees follow it)
+    hipStream_t lo = nullptr;  // normal priority: GEMMs, large draws and passes
+    hipStream_t hi = nullptr;  // high priority: the short dependent ops (reductions, casts, GEMV), or null
+    hipEvent_t hop = nullptr;  // orders the two streams when an op moves from one to the other
     void* ws = nullptr;
     void* scalar = nullptr;  // device fallback when no pinned slot exists
     double* slot = nullptr;
@@ -227,7 +230,18 @@ class HipDevice final : public broker::Device {
     }
     Ctx* c = new Ctx;
     hipSetDevice(0);
-    hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
+    hipStreamCreateWithFlags(&c->lo, hipStreamNonBlocking);
+    c->s = c->lo;
+    if (prio_) {
+      int least = 0, greatest = 0;
+      if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least &&
+          hipStreamCreateWithPriority(&c->hi, hipStreamNonBlocking, greatest) == hipSuccess &&
+          hipEventCreateWithFlags(&c->hop, hipEventDisableTiming) == hipSuccess) {
+      } else {
+        if (c->hi) hipStreamDestroy(c->hi);
+        c->hi = nullptr;
+      }
+    }
     bk.malloc_(&c->ws, bk.reduce_ws());
     bk.ws_init(c->ws, c->s);  // (ordered before every reduction on this stream)
     bk.malloc_(&c->scalar, 256);
@@ -270,6 +284,31 @@ class HipDevice final : public broker::Device {
   }
   static hipStream_t st(void* p) { return ((Ctx*)p)->s; }
 
+  // The stream for the session's next op.  Short ops -- reductions, casts,
+  // small passes, GEMV-sized products -- go to the high-priority stream, so
+  // the command processor dispatches them ahead of other sessions' queued
+  // GEMMs and large passes (under 8 concurrent sandboxes a 6 us row sum
+  // averaged 37 us and a 2.4 us reduction 19 us behind them,
+  // profiles/r3_final_served_kernels.csv).  One session's ops stay in issue
+  // order: moving to the other stream records an event on the one it leaves
+  // and makes the new one wait for it (GPU-side), and waits / deferred frees
+  // follow the latest stream (which by this chain follows everything before).
+  hipStream_t pick(void* p, bool short_op) {
+    Ctx* c = (Ctx*)p;
+    hipStream_t want = short_op && c->hi ? c->hi : c->lo;
+    if (want != c->s) {
+      if (hipEventRecord(c->hop, c->s) != hipSuccess || hipStreamWaitEvent(want, c->hop, 0) != hipSuccess) {
+        hipStreamSynchronize(c->s);  // (ordering by a host wait if the event path fails)
+      }
+      c->s = want;
+    }
+    return want;
+  }
+  // what counts as short: under ~16 MiB of memory traffic or ~2^31 flops
+  static constexpr int64_t kShortBytes = 16ll << 20;
+  static bool short_bytes(int64_t n, int64_t elem, int operands = 1) { return n * elem * operands <= kShortBytes; }
+  static int64_t elem_bytes(uint32_t dt) { return dt == 1 ? 8 : dt == 2 ? 2 : 4; }
+
   int malloc(void** p, uint64_t n) override { return bk.malloc_(p, (int64_t)n); }
   void free(void* p) override { bk.free_(p); }
   bool zero_async(void* p, uint64_t n, void* s) override { return hipMemsetAsync(p, 0, n, st(s)) == hipSuccess; }
@@ -285,20 +324,21 @@ class HipDevice final : public broker::Device {
   bool sync(void* s) override { return wait((Ctx*)s); }
   int rand(uint32_t kind, void* y, int64_t n, uint32_t dt, uint64_t seed, uint64_t off, double a, double b,
            void* s) override {
-    return kind == 0 ? bk.rand_uniform(y, n, (int)dt, seed, off, a, b, st(s)) : bk.rand_normal(y, n, (int)dt, seed, off, a, b, st(s));
+    hipStream_t q = pick(s, short_bytes(n, elem_bytes(dt)));
+    return kind == 0 ? bk.rand_uniform(y, n, (int)dt, seed, off, a, b, q) : bk.rand_normal(y, n, (int)dt, seed, off, a, b, q);
   }
   int unary(uint32_t op, uint32_t dt, const void* x, void* y, int64_t n, void* s) override {
-    return bk.unary((int)op, (int)dt, x, y, n, st(s));
+    return bk.unary((int)op, (int)dt, x, y, n, pick(s, short_bytes(n, elem_bytes(dt), 2)));
   }
   int binary(uint32_t op, uint32_t dt, uint32_t mode, const void* a, const void* b, double sc, void* y, int64_t n,
              void* s) override {
-    return bk.binary((int)op, (int)dt, (int)mode, a, b, sc, y, n, st(s));
+    return bk.binary((int)op, (int)dt, (int)mode, a, b, sc, y, n, pick(s, short_bytes(n, elem_bytes(dt), 3)));
   }
   int cast(uint32_t sdt, uint32_t ddt, const void* x, void* y, int64_t n, void* s) override {
-    return bk.cast((int)sdt, (int)ddt, x, y, n, st(s));
+    return bk.cast((int)sdt, (int)ddt, x, y, n, pick(s, short_bytes(n, elem_bytes(sdt) + elem_bytes(ddt))));
   }
   int fill(void* y, int64_t nbytes, uint64_t pattern, uint32_t width, void* s) override {
-    return bk.fill(y, nbytes, pattern, (int)width, st(s));
+    return bk.fill(y, nbytes, pattern, (int)width, pick(s, nbytes <= kShortBytes));
   }
   int fetch(Ctx* c, int rc, double* out) {
     if (rc != 0) return rc;
@@ -313,25 +353,28 @@ class HipDevice final : public broker::Device {
   }
   int reduce(uint32_t op, uint32_t dt, const void* a, const void* b, int64_t n, double* out, void* s) override {
     Ctx* c = (Ctx*)s;
-    return fetch(c, bk.reduce((int)op, (int)dt, a, b, n, c->ws, c->slot ? (void*)c->slot : c->scalar, c->s), out);
+    hipStream_t q = pick(s, short_bytes(n, elem_bytes(dt), b ? 2 : 1));
+    return fetch(c, bk.reduce((int)op, (int)dt, a, b, n, c->ws, c->slot ? (void*)c->slot : c->scalar, q), out);
   }
   int rand_reduce(uint32_t op, uint32_t dt, int64_t n, uint64_t seed, uint64_t off, double lo, double hi, double* out,
                   void* s) override {
     Ctx* c = (Ctx*)s;
-    return fetch(c, bk.rand_reduce((int)op, (int)dt, n, seed, off, lo, hi, c->ws, c->slot ? (void*)c->slot : c->scalar, c->s),
+    hipStream_t q = pick(s, n <= (1ll << 22));  // compute-bound: ~4 us per 4M values
+    return fetch(c, bk.rand_reduce((int)op, (int)dt, n, seed, off, lo, hi, c->ws, c->slot ? (void*)c->slot : c->scalar, q),
                  out);
   }
   int gemm(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
            float beta, int odt, void* s) override {
-    return bk.gemm(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, st(s));
+    return bk.gemm(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, pick(s, short_gemm(M, N, K)));
   }
   int gemm_nn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
               float beta, int odt, void* s) override {
     if (!bk.gemm_nn) return broker::kBadArgument;
-    return bk.gemm_nn(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, st(s));
+    return bk.gemm_nn(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, pick(s, short_gemm(M, N, K)));
   }
   int transpose(int sdt, int ddt, const void* in, void* out, int rows, int cols, int ldi, int ldo, void* s) override {
-    return bk.transpose(sdt, ddt, in, out, rows, cols, ldi, ldo, st(s));
+    return bk.transpose(sdt, ddt, in, out, rows, cols, ldi, ldo,
+                        pick(s, short_bytes((int64_t)rows * cols, elem_bytes(sdt) + elem_bytes(ddt))));
   }
   int reduce_axis(uint32_t op, uint32_t dt, const void* x, void* y, int64_t rows, int64_t cols, int64_t ld,
                   uint32_t axis, void* s) override {
@@ -341,7 +384,10 @@ class HipDevice final : public broker::Device {
       if (bk.malloc_(&c->axis_ws, bk.axis_ws()) != 0) return broker::kOutOfMemory;
       bk.axis_ws_init(c->axis_ws, c->s);
     }
-    return bk.reduce_axis((int)op, (int)dt, x, rows, cols, ld, (int)axis, y, c->axis_ws, c->s);
+    // a row / column sum reads the matrix once: ~64 MiB at 4096^2 f32 is
+    // ~10 us -- short next to the GEMM that produced it
+    return bk.reduce_axis((int)op, (int)dt, x, rows, cols, ld, (int)axis, y, c->axis_ws,
+                          pick(s, short_bytes(rows * ld, elem_bytes(dt)) || rows * ld <= (16ll << 20)));
   }
   const char* last_error() override { return bk.last_error ? bk.last_error() : ""; }
   void info(int64_t v[5]) override {
@@ -357,6 +403,10 @@ class HipDevice final : public broker::Device {
 
  private:
   bool spin_wait_ = getenv("BEE_BROKER_WAIT") && !strcmp(getenv("BEE_BROKER_WAIT"), "spin");
+  // BEE_BROKER_PRIO=0: one (normal-priority) stream per session, as before
+  bool prio_ = !(getenv("BEE_BROKER_PRIO") && !strcmp(getenv("BEE_BROKER_PRIO"), "0"));
+  // a GEMM whose work is a GEMV or a small product (<= 2^31 flops, ~2 us)
+  static bool short_gemm(int M, int N, int K) { return 2.0 * M * N * K <= 2147483648.0; }
   // default: relative backoff (2 us, then 1/8 of the wait so far, <= 50 us):
   // A/B on MI355X, 4 interleaved runs each, broker CPU 0.30-0.33 vs
   // 0.34-0.35 ms per Execute, RPS 2500-2665 vs 2466-2550
