@@ -97,6 +97,13 @@ def _preload() -> list:
             loaded.append("beekern")
         except Exception:
             pass
+    # the numpy offload (a request field): its modules pre-fork wherever
+    # numpy and beekern are, so a run that asks for it only patches numpy.random
+    if "numpy" in sys.modules and "bee_code_interpreter_fs_amd.ops" in sys.modules:
+        try:
+            from bee_code_interpreter_fs_amd.ops import npinterop, numpy_offload  # noqa: F401
+        except Exception:
+            pass
     # modules the worker's own code path imports lazily (stdlib), pre-fork
     for name in ("io", "types", "traceback", "linecache", "tokenize", "resource"):
         try:

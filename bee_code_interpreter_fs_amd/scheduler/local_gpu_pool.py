@@ -411,10 +411,16 @@ class LocalGpuPoolBackend(CodeExecutor):
                 code = precompiled_if_repeated(request.source_code)
                 if code is not None:
                     body["code"] = code
+            offload = self.config.numpy_offload if request.numpy_offload is None else request.numpy_offload
+            offload = bool(offload) and want > 0
             if not gang:
                 # CPU-only slots too: their executors keep minimal (numpy-only,
                 # fast-forking) and light zygotes as well
                 body["mode"] = sandbox_mode(request, self.storage)
+                if offload and body["mode"] == "min_cpu":
+                    # numpy code that will reach the GPU: a sandbox whose broker
+                    # session opened while it was pooled
+                    body["mode"] = "min"
             if gang:
                 body["gpus"] = ",".join(str(s.gpu) for s in slots)
                 body["nprocs"] = int(request.nprocs)
@@ -423,8 +429,7 @@ class LocalGpuPoolBackend(CodeExecutor):
                 body["gpus"] = ""  # CPU-only sandbox on a GPU slot
             if request.env:
                 body["env"] = dict(request.env)
-            offload = self.config.numpy_offload if request.numpy_offload is None else request.numpy_offload
-            if offload and want > 0:
+            if offload:
                 body["numpy_offload"] = True  # a job field: the pooled sandbox applies it (ops/numpy_offload.py)
             try:
                 resp = await lead.executor.post("/v1/execute", body, timeout=body["timeout"] + 180.0)

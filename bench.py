@@ -128,6 +128,8 @@ def parse_args():
                    help="CPU rehearsal of an N-GPU node: N executors pinned to GPU ids 0..N-1 that need not exist "
                         "(no kernel broker, no HIP warm-up); use with a CPU workload such as --workload hello")
     p.add_argument("--no-gang-check", action="store_true")
+    p.add_argument("--idle-probe", type=float, default=2.0,
+                   help="seconds of CPU sampling with the service idle (after READY, before the clients); 0 = skip")
     p.add_argument("--fold", action="store_true",
                    help="keep one executor daemon (broker, HIP context, pools) per requested GPU even when fewer GPUs "
                         "are visible: the N-GPU node's topology rehearsed on this box")
@@ -304,6 +306,58 @@ def pss_by_role(service_pid):
         roles[role] += pss
         stack.extend((c, role) for c in _children(pid))
     return {k: round(v, 1) for k, v in roles.items()}
+
+
+def daemon_threads(service_pid):
+    """CPU seconds so far of the executor daemons' threads, summed by thread
+    name (csrc/executor/util.cpp names them by role: http, refill, broker,
+    watchdog, ...) over every daemon of the service."""
+    out = {}
+    if service_pid is None:
+        return out
+    tck = os.sysconf("SC_CLK_TCK")
+    stack, seen = [service_pid], set()
+    while stack:
+        pid = stack.pop()
+        if pid in seen:
+            continue
+        seen.add(pid)
+        try:
+            with open(f"/proc/{pid}/cmdline", "rb") as f:
+                cmd = f.read()
+        except OSError:
+            continue
+        if b"bee-executor" not in cmd:
+            stack.extend(_children(pid))
+            continue
+        try:
+            tids = os.listdir(f"/proc/{pid}/task")
+        except OSError:
+            continue
+        for tid in tids:
+            try:
+                with open(f"/proc/{pid}/task/{tid}/stat") as f:
+                    raw = f.read()
+                name = raw[raw.index("(") + 1: raw.rindex(")")]
+                fields = raw.rsplit(")", 1)[1].split()
+                out[name] = out.get(name, 0.0) + (int(fields[11]) + int(fields[12])) / tck
+            except (OSError, ValueError):
+                continue
+    return out
+
+
+def idle_profile(service_pid, seconds: float):
+    """The service's CPU with no requests in flight (pools full, READY):
+    cores by role and the daemons' busiest threads -- fixed overhead that
+    every slot of the node pays whatever its load."""
+    r0, t0, c0 = cpu_by_role(service_pid), daemon_threads(service_pid), time.perf_counter()
+    time.sleep(seconds)
+    r1, t1, dt = cpu_by_role(service_pid), daemon_threads(service_pid), time.perf_counter() - c0
+    threads = {k: round((t1.get(k, 0.0) - v) / dt, 3) for k, v in t0.items()}
+    return {"seconds": round(dt, 2),
+            "cores_by_role": {k: round((r1[k] - r0[k]) / dt, 3) for k in r0 if k != "bench_clients"},
+            "daemon_thread_cores": dict(sorted(((k, v) for k, v in threads.items() if v > 0.001),
+                                               key=lambda kv: -kv[1])[:12])}
 
 
 def slot_executions(hport):
@@ -521,6 +575,7 @@ def run_loadgens(n_procs, targets, source, concurrency, warmup, steps, sync, mar
     if marks is not None:
         marks["t0"], marks["cpu0"] = time.perf_counter(), cpu_usage_s()[0]
         marks["roles0"] = cpu_by_role(marks.get("svc"))
+        marks["threads0"] = daemon_threads(marks.get("svc"))
         if marks.get("hport"):
             marks["slots0"] = slot_executions(marks["hport"])
     out = [results.get(timeout=3600) for _ in procs]
@@ -530,6 +585,7 @@ def run_loadgens(n_procs, targets, source, concurrency, warmup, steps, sync, mar
     if marks is not None:
         # (after the join: the load generators' CPU is then in our children's)
         marks["roles1"] = cpu_by_role(marks.get("svc"))
+        marks["threads1"] = daemon_threads(marks.get("svc"))
         if marks.get("hport"):
             marks["slots1"] = slot_executions(marks["hport"])
     return out
@@ -743,8 +799,11 @@ def main():
             dist.all_gather_object(allg, local)
             return [g for part in allg for g in part]
 
+        idle = None
         if rank == 0:
             wait_pools_ready(hport)
+            if args.idle_probe > 0:
+                idle = idle_profile(proc.pid, args.idle_probe)
         if world > 1:
             dist.barrier()
         cpu0, cpu_src = cpu_usage_s()
@@ -757,12 +816,14 @@ def main():
             cpu_busy = (cpu_usage_s()[0] - marks["cpu0"]) / max(time.perf_counter() - marks["t0"], 1e-9)
             roles0, roles1 = marks["roles0"], marks.get("roles1")
             slots0, slots1 = marks.get("slots0"), marks.get("slots1")
+            threads0, threads1 = marks.get("threads0"), marks.get("threads1")
         else:
             chans, stubs = loop.run_until_complete(open_clients(targets, first, args.concurrency))
             loop.run_until_complete(run_clients(stubs, source, args.warmup, extra=extra))  # warm every pool
             barrier()
             cpu0, cpu_src = cpu_usage_s()
             roles0 = cpu_by_role(svc_pid)
+            threads0 = daemon_threads(svc_pid)
             slots0 = slot_executions(hport) if rank == 0 else None
             trace = [] if os.environ.get("BEE_BENCH_TRACE") else None
             t0 = time.perf_counter()
@@ -771,6 +832,7 @@ def main():
             barrier()
             elapsed = time.perf_counter() - t0
             roles1 = cpu_by_role(svc_pid)
+            threads1 = daemon_threads(svc_pid)
             slots1 = slot_executions(hport) if rank == 0 else None
             cpu_busy = (cpu_usage_s()[0] - cpu0) / elapsed if elapsed > 0 else 0.0
             gathered = [(elapsed, lat, errors, exec_times, phases, checks)]
@@ -892,7 +954,13 @@ def main():
                 per["all_cgroup"] = round(cpu_busy * max_elapsed * 1e3 / total, 3)
                 per["unattributed"] = round(per["all_cgroup"] - sum(v for k, v in per.items() if k != "all_cgroup"), 3)
                 out["cpu_ms_per_exec"] = per
+                if threads0 and threads1:
+                    th = {k: round((threads1.get(k, 0.0) - v) * 1e3 / total, 3) for k, v in threads0.items()}
+                    out["daemon_threads_ms_per_exec"] = dict(sorted(((k, v) for k, v in th.items() if v > 0.0005),
+                                                                    key=lambda kv: -kv[1]))
             out["ready_s"] = round(ready_s, 2)
+            if idle is not None:
+                out["idle_cpu"] = idle
             # what bounds this node: the CPU quota over CPU per Execute is the
             # rate the service could reach with the GPUs idle; a run near it is
             # CPU-bound (more GPUs would not help), one well below it is set by

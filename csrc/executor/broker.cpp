@@ -407,11 +407,14 @@ class HipDevice final : public broker::Device {
   bool prio_ = !(getenv("BEE_BROKER_PRIO") && !strcmp(getenv("BEE_BROKER_PRIO"), "0"));
   // a GEMM whose work is a GEMV or a small product (<= 2^31 flops, ~2 us)
   static bool short_gemm(int M, int N, int K) { return 2.0 * M * N * K <= 2147483648.0; }
-  // default: relative backoff (2 us, then 1/8 of the wait so far, <= 50 us):
-  // A/B on MI355X, 4 interleaved runs each, broker CPU 0.30-0.33 vs
-  // 0.34-0.35 ms per Execute, RPS 2500-2665 vs 2466-2550
-  // (profiles/archive/r2_s3_broker_poll_ab.log)
-  long poll_min_ns_ = 2000, poll_max_ns_ = 50000;
+  // default: relative backoff (2 us, then 1/8 of the wait so far): A/B on
+  // MI355X, 4 interleaved runs each, broker CPU 0.30-0.33 vs 0.34-0.35 ms per
+  // Execute, RPS 2500-2665 vs 2466-2550 (profiles/archive/r2_s3_broker_poll_ab.log).
+  // The checks are capped at 500 us apart (was 50): a wait stays within 1/8
+  // of its length either way, and the long waits of a crowded GPU (8 slots
+  // folded onto one card: ~10 ms in-sandbox) no longer cost a check every
+  // 50 us -- 200 wake-ups per 10 ms wait, on every waiting session.
+  long poll_min_ns_ = 2000, poll_max_ns_ = 500000;
   int poll_div_ = 8;
   bool poll_set_ = (poll_schedule(&poll_min_ns_, &poll_max_ns_, &poll_div_), true);
   void* lib_ = nullptr;

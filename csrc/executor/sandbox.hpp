@@ -58,7 +58,7 @@ struct PoolConfig {
   int min_target = 0;                  // warm minimal sandboxes kept ready (0 = no minimal zygotes)
   int min_zygotes = 0;                 // parallel forkers for minimal sandboxes
   int min_cpu_target = -1;             // warm lazy-session minimal sandboxes (-1 = min_target; GPU pools only)
-  std::string min_preload = "numpy,bee_code_interpreter_fs_amd.ops";
+  std::string min_preload = "numpy,numpy.random,bee_code_interpreter_fs_amd.ops";
   int nano_target = 0;                 // warm numpy-free sandboxes kept ready (0 = no nano zygotes)
   int nano_zygotes = 0;                // parallel forkers for nano sandboxes
   int nano_cpu_target = -1;            // warm lazy-session nano sandboxes (-1 = nano_target; GPU pools only)
