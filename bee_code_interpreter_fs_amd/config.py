@@ -187,6 +187,12 @@ class Config:
     # (NCCL_MIN_NCHANNELS, NCCL_PROTO, ...) are left to RCCL's gfx950 tuning
     # tables unless set here for a measured reason
     gang_rccl_env: Dict[str, str] = field(default_factory=lambda: {"NCCL_IB_DISABLE": "1"})
+    # gang sizes kept warm on the node: for each size N, every aligned block
+    # of N GPU slots (all 8; 0-3 and 4-7; the pairs) has a rank set whose
+    # rank r already holds device r (HIP context + torch CUDA state) -- a
+    # gang request takes it like a pooled sandbox instead of forking N ranks
+    # and initialising HIP on the request path.  [] = every gang starts cold
+    gang_warm_sizes: List[int] = field(default_factory=lambda: [2, 4, 8])
     # processes + threads per sandbox tree (the executor's monitor, any
     # mode; plus RLIMIT_NPROC of the sandbox UID in UID mode)
     sandbox_max_processes: int = 1024

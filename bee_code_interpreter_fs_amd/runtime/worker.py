@@ -244,11 +244,21 @@ def warm_gpu() -> Optional[str]:
         from bee_code_interpreter_fs_amd import ops
 
         # BEE_BROKER_LAZY=1: a light/minimal sandbox opens its broker session
-        # on first use instead of while pooled
-        ops.init(0, lazy=os.environ.get("BEE_BROKER_LAZY") == "1")
+        # on first use instead of while pooled.  BEE_DEVICE: the device of a
+        # warm gang rank (rank r of a gang holds device r of its visible list)
+        device = int(os.environ.get("BEE_DEVICE", "0") or 0)
+        ops.init(device, lazy=os.environ.get("BEE_BROKER_LAZY") == "1")
         quota = int(os.environ.get("BEE_HBM_QUOTA_BYTES", "0") or 0)
         if quota > 0 and ops.driver_name() == "native":
             ops.set_quota(quota)
+        if os.environ.get("BEE_WARM_TORCH") == "1" and "torch" in sys.modules:
+            # torch's own CUDA state too (lazy init, the caching allocator's
+            # first block): a gang rank's `torch.cuda.set_device(LOCAL_RANK)`
+            # and first tensor then cost nothing on the request path
+            torch = sys.modules["torch"]
+            torch.cuda.set_device(device)
+            torch.zeros(1, device="cuda").add_(1)
+            torch.cuda.synchronize()
         return None
     except Exception as e:  # keep the sandbox usable for CPU code
         return f"{type(e).__name__}: {e}"

@@ -236,6 +236,7 @@ class LocalGpuPoolBackend(CodeExecutor):
                         "--nano-zygotes", str(c.nano_zygotes_per_gpu),
                         "--nano-cpu-target", str(c.nano_cpu_workers_per_gpu_target),
                         "--gang-grace", str(c.gang_failure_grace_s),
+                        "--gang-warm", ";".join(self._gang_keys_led_by(i)),
                         "--gang-env", ",".join(f"{k}={v}" for k, v in sorted((c.gang_rccl_env or {}).items())
                                                if "," not in f"{k}={v}"),
                         # admission for every front-end replica of the node
@@ -248,6 +249,29 @@ class LocalGpuPoolBackend(CodeExecutor):
                         "--cgroup", c.sandbox_cgroup or "auto", "--cgroup-root", c.sandbox_cgroup_root or "",
                         *isolation_args(c, i, [self.storage.storage_path])],
         )
+
+    def _aligned_blocks(self, n: int) -> List[List[int]]:
+        """Slot-index blocks a gang of ``n`` is placed on first: aligned runs
+        of n slots (all 8; 0-3 / 4-7; the pairs), each over n distinct GPUs."""
+        ids = list(self.gpu_ids)
+        out = []
+        for i in range(0, len(ids) - n + 1, n):
+            block = list(range(i, i + n))
+            if len({ids[j] for j in block}) == n:
+                out.append(block)
+        return out
+
+    def _gang_keys_led_by(self, slot: int) -> List[str]:
+        """The warm gang sets slot ``slot``'s daemon keeps: the aligned blocks
+        it leads (their first slot), as the GPU list a gang request names."""
+        if not self.gpu_ids or slot >= len(self.gpu_ids):
+            return []
+        keys = []
+        for n in sorted({int(x) for x in (self.config.gang_warm_sizes or []) if 1 < int(x) <= len(self.gpu_ids)}):
+            for block in self._aligned_blocks(n):
+                if block[0] == slot:
+                    keys.append(",".join(str(self.gpu_ids[j]) for j in block))
+        return keys
 
     async def wait_ready(self, timeout: float = 300.0) -> None:
         await asyncio.gather(*(s.executor.wait_ready(min(1, self.config.workers_per_gpu_target), timeout) for s in self.slots))
@@ -333,7 +357,17 @@ class LocalGpuPoolBackend(CodeExecutor):
                 if len(free) >= n:
                     break
                 await self._cond.wait()
-            gang = sorted(free, key=lambda s: (s.inflight, s.index))[:n]
+            # an aligned block first (its lead daemon keeps a warm rank set
+            # for it, config.gang_warm_sizes), the least busy one; any n
+            # healthy slots otherwise
+            free_ix = {s.index for s in free}
+            blocks = [b for b in self._aligned_blocks(n) if all(i in free_ix for i in b)]
+            if blocks:
+                by_ix = {s.index: s for s in free}
+                best = min(blocks, key=lambda b: (sum(by_ix[i].inflight for i in b), b[0]))
+                gang = [by_ix[i] for i in best]
+            else:
+                gang = sorted(free, key=lambda s: (s.inflight, s.index))[:n]
             for s in gang:
                 s.reserved = True
             try:

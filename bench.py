@@ -620,7 +620,21 @@ dist.destroy_process_group()
 """
 
 
-def gang_allreduce_check(target, n, repeats=2):
+def _gang_warm_state(hport, n):
+    """(warm-set state of the aligned n-GPU block led by slot 0, warm hits,
+    cold starts) from the service's status."""
+    import urllib.request
+
+    try:
+        with urllib.request.urlopen(f"http://127.0.0.1:{hport}/v1/status", timeout=10) as f:
+            e = json.load(f)["slots"][0]["executor"]
+        key = ",".join(str(i) for i in range(n))
+        return (e.get("gang_warm") or {}).get(key), e.get("gang_warm_hits"), e.get("gang_cold_starts")
+    except Exception:  # noqa: BLE001
+        return None, None, None
+
+
+def gang_allreduce_check(target, n, repeats=2, hport=None):
     """BASELINE config 5: an N-GPU torch.distributed (RCCL) job inside one
     gang sandbox, dispatched through the service like any other request --
     ``repeats`` back to back, each timed end to end (the ranks are spawned
@@ -637,9 +651,28 @@ def gang_allreduce_check(target, n, repeats=2):
         with grpc.insecure_channel(target) as ch:
             stub = pb.CodeInterpreterServiceStub(ch)
             for _ in range(repeats):
+                # the gang's warm rank set (config.gang_warm_sizes): wait for it
+                # to be ready, so the run measures the warm path (the state
+                # and the wait are reported; a cold start says so)
+                state, waited = None, time.perf_counter()
+                if hport:
+                    deadline = time.monotonic() + 60
+                    while time.monotonic() < deadline:
+                        state, _, _ = _gang_warm_state(hport, n)
+                        if state in ("ready", None):
+                            break
+                        time.sleep(0.2)
+                _, hits0, cold0 = _gang_warm_state(hport, n) if hport else (None, None, None)
                 t = time.perf_counter()
                 r = stub.Execute(pb.ExecuteRequest(source_code=GANG_SCRIPT, gpus=n, timeout=180), timeout=240)
-                run = {"exit_code": r.exit_code, "latency_ms": round((time.perf_counter() - t) * 1e3, 1)}
+                run = {"exit_code": r.exit_code, "latency_ms": round((time.perf_counter() - t) * 1e3, 1),
+                       "warm_set": state, "warm_wait_s": round(t - waited, 2),
+                       "acquire_ms": round(r.timings_ms.get("acquire", -1.0), 1),
+                       "queue_ms": round(r.timings_ms.get("queue", -1.0), 1)}
+                if hport:
+                    _, hits1, cold1 = _gang_warm_state(hport, n)
+                    if hits0 is not None and hits1 is not None:
+                        run["rank_start"] = "warm" if hits1 > hits0 else "cold" if cold1 > cold0 else "?"
                 line = [l for l in r.stdout.splitlines() if l.startswith("allreduce_ok")]
                 if line:
                     kv = dict(p.split("=", 1) for p in line[0].split())
@@ -886,7 +919,7 @@ def main():
             # (a gang needs n distinct GPUs: RCCL refuses two ranks on one
             # device, so a folded rehearsal skips it)
             gang = (
-                gang_allreduce_check(target, n_gpus)
+                gang_allreduce_check(target, n_gpus, hport=hport)
                 if n_gpus > 1 and not args.no_gang_check and not args.cpu_only and len(set(ids)) >= n_gpus
                 else None
             )

@@ -159,6 +159,16 @@ int main(int argc, char** argv) {
         i = j + 1;
       }
     }
+    else if (a == "--gang-warm") {  // "0,1,2,3;0,1": gang GPU lists this daemon leads
+      const std::string spec = val();
+      size_t i = 0;
+      while (i < spec.size()) {
+        size_t j = spec.find(';', i);
+        if (j == std::string::npos) j = spec.size();
+        if (j > i) cfg.gang_warm.push_back(spec.substr(i, j - i));
+        i = j + 1;
+      }
+    }
     else if (a == "--hbm-watchdog-ms") cfg.hbm_watchdog_ms = atoi(val().c_str());
     else if (a == "--hbm-slack") cfg.hbm_slack = atoll(val().c_str());
     else if (a == "--max-inflight") cfg.max_inflight = atoi(val().c_str());

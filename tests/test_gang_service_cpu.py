@@ -95,3 +95,29 @@ def test_gang_reinitialises_process_group(two_slot_service):
     assert r.exit_code == 0, r.stderr
     for k in range(3):
         assert r.stdout.count(f"round{k} ") == 2 and f"sum={3.0 + 2 * k}" in r.stdout, r.stdout
+
+
+def _slot_status(h, i=0):
+    return h.call(h.ctx.code_executor.slots[i].executor.get_json("/v1/status"), timeout=30)
+
+
+def test_gang_ranks_come_from_the_warm_set(two_slot_service):
+    """The lead daemon of an aligned block keeps a warm rank set for it
+    (config.gang_warm_sizes): a gang request takes it -- no rank is forked
+    on the request path -- and a new set is warmed behind it; while none is
+    ready, a gang starts cold as before."""
+    import time
+
+    h = two_slot_service
+    deadline = time.time() + 90
+    while _slot_status(h)["gang_warm"].get("0,1") != "ready" and time.time() < deadline:
+        time.sleep(0.2)
+    st = _slot_status(h)
+    assert st["gang_warm"] == {"0,1": "ready"}, st["gang_warm"]
+    assert _slot_status(h, 1)["gang_warm"] == {}  # slot 1 leads no aligned block
+    hits, cold = st["gang_warm_hits"], st["gang_cold_starts"]
+    r = h.call(h.ctx.code_executor.execute(source_code=GANG_GLOO, gpus=2, nprocs=2, timeout=120), timeout=300)
+    assert r.exit_code == 0 and r.stdout.count("sum=3.0") == 2, (r.stdout, r.stderr)
+    st = _slot_status(h)
+    assert st["gang_warm_hits"] == hits + 1 and st["gang_cold_starts"] == cold, st
+    assert r.timings_ms["acquire"] < 100.0, r.timings_ms  # no fork + warm-up on the request path

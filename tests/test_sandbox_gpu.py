@@ -409,3 +409,25 @@ def test_cuda_tensor_sharing_between_a_sandboxs_processes(gsvc):
     r = run(gsvc, code, timeout=120)
     assert r.exit_code == 0, r.stderr[-2000:]
     assert r.stdout.strip() == "4096.0", r.stdout
+
+
+def test_warm_gang_rank_holds_torch_state_on_its_device(gpu):
+    """What a warm gang rank does while pooled (BEE_WARM_GPU + BEE_WARM_TORCH,
+    BEE_DEVICE = its rank): beekern's HIP context and torch's CUDA state on
+    that device, so the rank's torch.cuda.set_device(LOCAL_RANK) and first
+    tensor cost nothing on the request path.  (Gangs themselves need the
+    8-GPU node: tests/test_gang_gpu.py.)"""
+    import os
+    import subprocess
+    import sys
+
+    code = ("import torch\n"
+            "from bee_code_interpreter_fs_amd.runtime import worker\n"
+            "err = worker.warm_gpu()\n"
+            "print(err, torch.cuda.is_initialized(), torch.cuda.current_device(), torch.cuda.memory_allocated() > 0)\n")
+    env = dict(os.environ, BEE_WARM_GPU="1", BEE_WARM_TORCH="1", BEE_DEVICE="0", HIP_VISIBLE_DEVICES="0")
+    env.pop("BEE_BROKER_SOCK", None)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.stdout.split()[-4:] == ["None", "True", "0", "True"], p.stdout
