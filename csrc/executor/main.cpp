@@ -57,7 +57,7 @@ void usage() {
           "                    [--jail 0|1] [--uid-base UID] [--uid-count N] [--protect DIR]... [--nproc N]\n"
           "                    [--mem-limit BYTES] [--cpus LIST] [--gang-grace S]\n"
           "                    [--hbm-watchdog-ms MS] [--hbm-slack BYTES] [--max-inflight N] [--hbm-capacity BYTES]\n"
-          "                    [--admit-timeout S] [--sandbox-memory BYTES] [--sandbox-tasks N] [--sandbox-cpus C]\n"
+          "                    [--admit-timeout S] [--mem-capacity BYTES] [--sandbox-memory BYTES] [--sandbox-tasks N] [--sandbox-cpus C]\n"
           "                    [--monitor-ms MS] [--deny-ports P1,P2,...]\n"
           "                    [--cgroup auto|require|off|fake] [--cgroup-root DIR]\n");
 }
@@ -173,6 +173,7 @@ int main(int argc, char** argv) {
     else if (a == "--hbm-slack") cfg.hbm_slack = atoll(val().c_str());
     else if (a == "--max-inflight") cfg.max_inflight = atoi(val().c_str());
     else if (a == "--hbm-capacity") cfg.hbm_capacity = atoll(val().c_str());
+    else if (a == "--mem-capacity") cfg.mem_capacity = atoll(val().c_str());
     else if (a == "--admit-timeout") cfg.admit_timeout_s = atof(val().c_str());
     else if (a == "--sandbox-memory") cfg.sandbox_mem_bytes = atoll(val().c_str());
     else if (a == "--sandbox-tasks") cfg.sandbox_tasks = atoll(val().c_str());

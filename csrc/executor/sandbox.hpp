@@ -88,6 +88,10 @@ struct PoolConfig {
   // the rest wait in arrival order (or get a 429 when they asked not to wait)
   int max_inflight = 0;                // 0 = unbounded
   int64_t hbm_capacity = 0;            // bytes; 0 = unbounded
+  // this daemon's share of the node's host memory for sandbox trees: each
+  // admitted job commits its trees' memory bound (sandbox_mem_bytes x ranks),
+  // the commitments stay within it and the rest queue (0 = unbounded)
+  int64_t mem_capacity = 0;
   double admit_timeout_s = 900.0;      // longest wait for admission (then 503)
   // per-sandbox containment, what the reference pod's container resources
   // bound (procmon.hpp): the whole process tree of a sandbox
@@ -318,6 +322,7 @@ class SandboxPool {
   bool min_ok_ = false;    // minimal zygotes running
   bool nano_ok_ = false;   // nano (numpy-free) zygotes running
   int64_t jobs_ = 0;            // admitted jobs (guarded by mu_)
+  int64_t mem_committed_ = 0, max_mem_seen_ = 0;  // host-memory bounds of the admitted jobs' trees
   int64_t hbm_committed_ = 0;   // their HBM quotas
   int64_t max_jobs_seen_ = 0, max_hbm_seen_ = 0, admitted_ = 0;
   uint64_t admit_next_ = 0;     // admission tickets, served in order
