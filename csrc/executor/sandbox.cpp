@@ -1504,9 +1504,10 @@ Json SandboxPool::run_job(const Json& req, int* http_status, bool pod) {
   // bound (the monitor kills it above), so that is what admission commits
   const int64_t job_ranks = std::max<int64_t>(1, req["nprocs"].as_int(1));
   const int64_t job_mem = cfg_.sandbox_mem_bytes > 0 ? cfg_.sandbox_mem_bytes * job_ranks : 0;
-  if (cfg_.mem_capacity > 0 && job_mem > cfg_.mem_capacity)
-    return fail(400, "the job's sandbox memory bound (" + std::to_string(job_mem >> 20) + " MiB) exceeds this slot's " +
-                         "host-memory capacity (" + std::to_string(cfg_.mem_capacity >> 20) + " MiB)");
+  // (a gang's ranks run on as many slots, each drained for it: N shares)
+  if (cfg_.mem_capacity > 0 && job_mem > cfg_.mem_capacity * job_ranks)
+    return fail(400, "the job's sandbox memory bound (" + std::to_string(job_mem >> 20) + " MiB) exceeds its slots' " +
+                         "host-memory capacity (" + std::to_string((cfg_.mem_capacity * job_ranks) >> 20) + " MiB)");
   const bool try_only = req["admit"].str_or("wait") == "try";
   {
     std::unique_lock<std::mutex> lk(mu_);
