@@ -403,8 +403,14 @@ class HipDevice final : public broker::Device {
 
  private:
   bool spin_wait_ = getenv("BEE_BROKER_WAIT") && !strcmp(getenv("BEE_BROKER_WAIT"), "spin");
-  // BEE_BROKER_PRIO=0: one (normal-priority) stream per session, as before
-  bool prio_ = !(getenv("BEE_BROKER_PRIO") && !strcmp(getenv("BEE_BROKER_PRIO"), "0"));
+  // BEE_BROKER_PRIO=1: short ops on a high-priority stream (pick()).  Off by
+  // default: measured on MI355X (300 served headline Executes, 8 concurrent,
+  // profiles/r4_served_prio_ab.md) the high-priority queue let reductions
+  // start beside other sessions' GEMMs instead of after them, where they ran
+  // slower and slowed the GEMMs: bk.reduce 181 vs 126 us and bk.rand_reduce
+  // 525 vs 423 us per op, rowsum 39 vs 32 us per kernel, 2763-2835 vs
+  // 2815-2880 RPS, +0.15 ms daemon CPU per Execute (the stream hops).
+  bool prio_ = getenv("BEE_BROKER_PRIO") && !strcmp(getenv("BEE_BROKER_PRIO"), "1");
   // a GEMM whose work is a GEMV or a small product (<= 2^31 flops, ~2 us)
   static bool short_gemm(int M, int N, int K) { return 2.0 * M * N * K <= 2147483648.0; }
   // default: relative backoff (2 us, then 1/8 of the wait so far): A/B on

@@ -36,14 +36,16 @@ def test_payload_runs_on_pinned_gpu(gsvc):
 def test_nano_sandbox_runs_beekern_without_numpy(gsvc):
     """A beekern + stdlib script lands in a nano sandbox (zygote without
     numpy, python -S): the broker path works, reductions come back as plain
-    floats, numpy is never imported -- and a script that asks for numpy
-    afterwards still gets numpy.float64 results."""
+    floats, numpy is never imported -- and once beekern needs numpy (a
+    download) the reductions come back as numpy.float64.  (A script with a
+    dynamic import -- __import__, importlib -- is routed to a site-enabled
+    sandbox instead: tests/test_units.py test_sandbox_mode_routing.)"""
     code = (
         "import sys, beekern as bk\n"
         "x = bk.random.rand(1 << 20)\n"
         "s = bk.sum(bk.square(x))\n"
         "print(round(s / (1 << 20), 2), type(s).__name__, 'numpy' in sys.modules, sys.flags.no_site, bk.driver_name())\n"
-        "np = __import__('num' + 'py')\n"
+        "_ = x.numpy()\n"  # beekern imports numpy on first use (ops/_lazy.py)
         "print(type(bk.sum(x)).__name__)\n"
     )
     r = run(gsvc, code)
