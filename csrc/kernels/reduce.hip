@@ -12,6 +12,8 @@
 // launch used to do the fold: under concurrent sandboxes it queued behind
 // other tenants' GEMMs holding every CU -- 25 us mean for a 1.8 us kernel,
 // profiles/archive/r2_s3_final_served_path_kernels.csv.)
+#include <cstring>
+
 #include "bk_common.hpp"
 #include "bk_philox.hpp"
 
@@ -226,6 +228,68 @@ __global__ __launch_bounds__(kRedBlock) void reduce_1pass(const T* __restrict__ 
   finish<OP>(block_reduce<OP>(v), partials, ticket, out);
 }
 
+// Block-contiguous layout: block b owns one contiguous run of the array and
+// its lanes walk it 16 vectors (64 KiB per 256-lane block) at a time, so a
+// block's 16 loads in flight are consecutive 4 KiB stripes.  The grid-stride
+// layout above puts a lane's 16 loads gridDim x 4 KiB apart (32 MiB at 8192
+// blocks) -- every wave of the chip then hits the same few power-of-two
+// address strides at once (a channel-camping pattern); here the concurrent
+// reads are spread over the whole array.  BK_REDUCE_LAYOUT=stride keeps the
+// grid-stride kernel (A/B: tools/reduce_sweep.py).
+template <typename T, int OP, bool NT>
+__global__ __launch_bounds__(kRedBlock) void reduce_chunked(const T* __restrict__ a, const T* __restrict__ b,
+                                                           int64_t n, double* __restrict__ partials,
+                                                           unsigned* __restrict__ ticket, double* __restrict__ out) {
+  using V = V16<T>;
+  constexpr int N = 16 / sizeof(T);
+  constexpr int U = kRedUnroll;
+  const int64_t nvec = n / N;
+  // runs of whole 256-vector stripes, the last block takes what is left
+  const int64_t stripes = (nvec + kRedBlock - 1) / kRedBlock;
+  const int64_t per = (stripes + gridDim.x - 1) / gridDim.x;
+  const int64_t v0 = (int64_t)blockIdx.x * per * kRedBlock;
+  const int64_t v1 = v0 + per * kRedBlock < nvec ? v0 + per * kRedBlock : nvec;
+  double acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = red_init<OP>();
+  int64_t i = v0 + threadIdx.x;
+  for (; i + (int64_t)(U - 1) * kRedBlock < v1; i += (int64_t)U * kRedBlock) {
+    V va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      va[u] = ld16<NT>(reinterpret_cast<const V*>(a) + i + u * kRedBlock);
+      if constexpr (kTwoOperands<OP>) vb[u] = ld16<NT>(reinterpret_cast<const V*>(b) + i + u * kRedBlock);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const double bj = kTwoOperands<OP> ? to_f64<T>(vb[u].v[j]) : 0.0;
+        acc[u] = red_combine<OP>(acc[u], red_map<OP>(to_f64<T>(va[u].v[j]), bj));
+      }
+  }
+  for (; i < v1; i += kRedBlock) {
+    V va = ld16<NT>(reinterpret_cast<const V*>(a) + i);
+    V vb;
+    if constexpr (kTwoOperands<OP>) vb = ld16<NT>(reinterpret_cast<const V*>(b) + i);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const double bj = kTwoOperands<OP> ? to_f64<T>(vb.v[j]) : 0.0;
+      acc[0] = red_combine<OP>(acc[0], red_map<OP>(to_f64<T>(va.v[j]), bj));
+    }
+  }
+  // the scalar tail (n % N elements) in the last block
+  if (blockIdx.x == gridDim.x - 1)
+    for (int64_t k = nvec * N + threadIdx.x; k < n; k += kRedBlock) {
+      const double bk_ = kTwoOperands<OP> ? to_f64<T>(b[k]) : 0.0;
+      acc[0] = red_combine<OP>(acc[0], red_map<OP>(to_f64<T>(a[k]), bk_));
+    }
+  double v = acc[0];
+#pragma unroll
+  for (int u = 1; u < U; ++u) v = red_combine<OP>(v, acc[u]);
+  finish<OP>(block_reduce<OP>(v), partials, ticket, out);
+}
+
 // ---- fused RNG -> reduce -------------------------------------------------------
 // sum / square-sum over a uniform Philox stream WITHOUT materialising it:
 // element i takes exactly the value philox_uniform_{f64,f32} would store
@@ -298,10 +362,16 @@ int launch_reduce(const void* a, const void* b, int64_t n, double* workspace, do
   unsigned g = stream_grid(lanes_needed > 0 ? lanes_needed : 1, kRedBlock, (int)(red_blocks / kNumCU));
   if (g > (unsigned)red_blocks) g = (unsigned)red_blocks;  // the workspace holds kRedMaxBlocks partials
   unsigned* ticket = reinterpret_cast<unsigned*>(workspace + kRedMaxBlocks);
-  if (stream_nt(n * (int64_t)sizeof(T) * (kTwoOperands<OP> ? 2 : 1)))
+  static const bool chunked = !(getenv("BK_REDUCE_LAYOUT") && !strcmp(getenv("BK_REDUCE_LAYOUT"), "stride"));
+  const bool nt = stream_nt(n * (int64_t)sizeof(T) * (kTwoOperands<OP> ? 2 : 1));
+  if (chunked) {
+    if (nt) reduce_chunked<T, OP, true><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
+    else reduce_chunked<T, OP, false><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
+  } else if (nt) {
     reduce_1pass<T, OP, true><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
-  else
+  } else {
     reduce_1pass<T, OP, false><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
+  }
   return launch_status();
 }
 

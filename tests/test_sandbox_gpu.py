@@ -71,16 +71,18 @@ def test_light_and_direct_sandboxes(gsvc):
 
 
 def test_lazy_session_sandbox_can_still_use_the_gpu(gsvc):
-    """A script with no GPU import is routed to a min_cpu sandbox (broker
-    session opened on first use); reaching beekern dynamically still works,
-    and the executor really served it from that pool."""
+    """A script with no GPU import is routed to a lazy-session sandbox
+    (nano_cpu: broker session opened on first use); reaching beekern anyway
+    -- here the module its zygote preloaded, through sys.modules -- still
+    works, and the executor really served it from that pool.  (importlib /
+    __import__ would route the script to a site-enabled light sandbox.)"""
     import asyncio
 
     before = asyncio.run_coroutine_threadsafe(gsvc.ctx.code_executor.status(), gsvc.loop).result(30)
     code = (
-        "import importlib, os\n"
+        "import os, sys\n"
         "print(os.environ.get('BEE_BROKER_LAZY'))\n"
-        "bk = importlib.import_module('bee' + 'kern')\n"
+        "bk = sys.modules['bee' + 'kern']\n"
         "print(round(float(bk.sum(bk.square(bk.random.rand(1 << 20)))) / (1 << 20), 2), bk.driver_name())\n"
     )
     r = run(gsvc, code)

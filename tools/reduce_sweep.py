@@ -27,7 +27,7 @@ x = bk.random.default_rng(1).random(n)   # materialised f64
 def once():
     if what == "square_sum":
         return bk.square_sum(x)
-    bk.driver().rand(0, x.ptr, n, x.code, 7, 0, 0.0, 1.0)
+    sys.modules["bee_code_interpreter_fs_amd.ops.array"].driver().rand(0, x.ptr, n, x.code, 7, 0, 0.0, 1.0)
 for _ in range(3):
     once()
 bk.synchronize()
@@ -57,8 +57,9 @@ def main():
     ap.add_argument("--n", type=int, default=10**8)
     ap.add_argument("--reps", type=int, default=30)
     a = ap.parse_args()
-    for blocks in (2048, 4096, 8192, 12288, 16384, 24576, 32768):
-        run("square_sum", {"BK_REDUCE_BLOCKS": str(blocks)}, a.n, a.reps)
+    for layout in ("chunk", "stride"):  # reduce.hip reduce_chunked vs reduce_1pass
+        for blocks in (1024, 2048, 4096, 8192, 16384):
+            run("square_sum", {"BK_REDUCE_BLOCKS": str(blocks), "BK_REDUCE_LAYOUT": layout}, a.n, a.reps)
     run("philox_store", {}, a.n, a.reps)  # (its grid is fixed: kDrawBlocksPerCU, profiles/archive/r3_philox_grid_sweep.log)
 
 
