@@ -39,7 +39,11 @@ constexpr int kRedBlock = 256;
 // (the workspace holds kRedMaxBlocks partials; the default grid is
 // kRedBlocks, BK_REDUCE_BLOCKS overrides it up to the workspace for sweeps)
 constexpr int kRedMaxBlocks = 32768;
-constexpr int kRedBlocks = 8192;
+// 1024 blocks (4 per CU) with the block-contiguous layout: tools/reduce_sweep.py
+// on MI355X, 1e8 f64 square-sum, median of 30: 153 / 157 / 157 / 177 / 265 us
+// at 1024 / 2048 / 4096 / 8192 / 16384 blocks (the grid-stride layout 161 /
+// 170 / 174 / 178 / 249; profiles/r4_reduce_sweep.jsonl)
+constexpr int kRedBlocks = 1024;
 constexpr int kRedUnroll = 16;
 // the fused RNG->reduce kernels are compute-bound: 4 blocks per CU
 constexpr int kRandRedMaxBlocks = 1024;

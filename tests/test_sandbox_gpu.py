@@ -428,7 +428,7 @@ def test_warm_gang_rank_holds_torch_state_on_its_device(gpu):
     code = ("import torch\n"
             "from bee_code_interpreter_fs_amd.runtime import worker\n"
             "err = worker.warm_gpu()\n"
-            "print(err, torch.cuda.is_initialized(), torch.cuda.current_device(), torch.cuda.memory_allocated() > 0)\n")
+            "print(err, torch.cuda.is_initialized(), torch.cuda.current_device(), torch.cuda.memory_reserved() > 0)\n")
     env = dict(os.environ, BEE_WARM_GPU="1", BEE_WARM_TORCH="1", BEE_DEVICE="0", HIP_VISIBLE_DEVICES="0")
     env.pop("BEE_BROKER_SOCK", None)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

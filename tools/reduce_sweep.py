@@ -24,15 +24,28 @@ bk.init(0)
 n, reps, what = {n}, {reps}, {what!r}
 bk.set_lazy_random(False)
 x = bk.random.default_rng(1).random(n)   # materialised f64
+if what in ("torch_sum", "d2d_copy"):
+    import torch
+    tx = torch.rand(n, dtype=torch.float64, device="cuda")
+    ty = torch.empty_like(tx)
 def once():
     if what == "square_sum":
         return bk.square_sum(x)
+    if what == "torch_sum":
+        return tx.sum()
+    if what == "d2d_copy":
+        return ty.copy_(tx)
     sys.modules["bee_code_interpreter_fs_amd.ops.array"].driver().rand(0, x.ptr, n, x.code, 7, 0, 0.0, 1.0)
 for _ in range(3):
     once()
 bk.synchronize()
 ts = []
 for _ in range(reps):
+    if what in ("torch_sum", "d2d_copy"):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(); once(); e.record(); torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e))
+        continue
     with bk.Timer() as t:
         once()
     ts.append(t.ms)
@@ -60,7 +73,9 @@ def main():
     for layout in ("chunk", "stride"):  # reduce.hip reduce_chunked vs reduce_1pass
         for blocks in (1024, 2048, 4096, 8192, 16384):
             run("square_sum", {"BK_REDUCE_BLOCKS": str(blocks), "BK_REDUCE_LAYOUT": layout}, a.n, a.reps)
-    run("philox_store", {}, a.n, a.reps)  # (its grid is fixed: kDrawBlocksPerCU, profiles/archive/r3_philox_grid_sweep.log)
+    run("philox_store", {}, a.n, a.reps)
+    run("torch_sum", {}, a.n, a.reps)   # torch's own reduction over the same 800 MB (read roofline reference)
+    run("d2d_copy", {}, a.n, a.reps)    # hipMemcpy device-to-device: 800 MB read + 800 MB written  # (its grid is fixed: kDrawBlocksPerCU, profiles/archive/r3_philox_grid_sweep.log)
 
 
 if __name__ == "__main__":
