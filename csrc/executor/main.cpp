@@ -174,6 +174,7 @@ int main(int argc, char** argv) {
     else if (a == "--max-inflight") cfg.max_inflight = atoi(val().c_str());
     else if (a == "--hbm-capacity") cfg.hbm_capacity = atoll(val().c_str());
     else if (a == "--mem-capacity") cfg.mem_capacity = atoll(val().c_str());
+    else if (a == "--sandbox-network") cfg.sandbox_network = val();
     else if (a == "--admit-timeout") cfg.admit_timeout_s = atof(val().c_str());
     else if (a == "--sandbox-memory") cfg.sandbox_mem_bytes = atoll(val().c_str());
     else if (a == "--sandbox-tasks") cfg.sandbox_tasks = atoll(val().c_str());
