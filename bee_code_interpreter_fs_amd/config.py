@@ -173,10 +173,13 @@ class Config:
     # with a CPU quota far below the CPUs the job may run on (cgroup cpu.max:
     # 16 CPUs of time on a 256-CPU host), pin the service to this many times
     # the quota's worth of CPUs, split between the GPU slots (0 = NUMA only).
-    # Off by default: on the MI355X box 2x cut CPU per Execute 15-20% but not
-    # latency -- driver-length runs 1802-2224 vs 2010-2189 RPS, 600-step runs
-    # 1938 / 2443 vs 2343 / 2561 (profiles/r3_cpu_quota_pinning_ab.log)
-    cpu_quota_pin_factor: float = 0.0
+    # 8: each slot's daemon, zygotes and sandboxes keep to their own CPUs.
+    # Measured on MI355X with 8 slots folded onto one GPU and a 16-CPU quota
+    # (bench.py --gpus 8 --fold, profiles/r4_fold_rehearsal.md): 0 -> 2402 RPS
+    # at 6.3 ms CPU per Execute, 2 -> 972 (4 CPUs a slot starve its zygotes),
+    # 4 -> 1939, 8 -> 3416 RPS at 4.0 ms (the 1-slot run's 4.2); one slot:
+    # 2x cut CPU 15-20% but not latency (profiles/archive/r3_cpu_quota_pinning_ab.log)
+    cpu_quota_pin_factor: float = 8.0
     # a gang whose rank failed: seconds the other ranks get to finish before
     # the whole gang is killed (they are usually stuck in a collective)
     gang_failure_grace_s: float = 10.0

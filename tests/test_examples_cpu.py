@@ -221,19 +221,21 @@ def test_sandbox_environment_is_one_view(stub):
 def test_beekern_only_script_runs_numpy_free(stub):
     """A script importing only beekern + stdlib is served by a sandbox whose
     zygote never imported numpy (executor kind "nano"): numpy is not in
-    sys.modules until the script itself asks for it, and then it still
-    imports (ops/_lazy.py): the zygote ran without `site` start-up hooks
-    (python -S) yet site-packages stay importable."""
+    sys.modules until beekern needs it, and then it still imports
+    (ops/_lazy.py): the zygote ran without `site` start-up hooks (python -S)
+    yet site-packages stay importable.  (A script importing dynamically --
+    __import__, importlib -- goes to a site-enabled sandbox instead.)"""
     src = (
         "import sys, time\n"
         "import beekern as bk\n"
         "print('numpy' in sys.modules, bk.__name__, sys.flags.no_site, 'certifi' in sys.modules)\n"
-        "np = __import__('num' + 'py')\n"
+        "print(bk.normalize_dtype(float))\n"  # beekern imports numpy on first use (ops/_lazy.py)
+        "np = sys.modules['numpy']\n"
         "print(np.float64(2.5) * 2)\n"
     )
     r = stub.Execute(pb.ExecuteRequest(source_code=src), timeout=120)
     assert r.exit_code == 0, r.stderr
-    assert r.stdout.split("\n")[:2] == ["False bee_code_interpreter_fs_amd.ops 1 False", "5.0"], r.stdout
+    assert r.stdout.split("\n")[:3] == ["False bee_code_interpreter_fs_amd.ops 1 False", "float64", "5.0"], r.stdout
     r = stub.Execute(pb.ExecuteRequest(source_code="import sys\nimport numpy, beekern\nprint('numpy' in sys.modules)\n"),
                      timeout=120)
     assert (r.exit_code, r.stdout) == (0, "True\n"), r.stderr
