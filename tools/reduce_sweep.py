@@ -71,7 +71,7 @@ def main():
     ap.add_argument("--reps", type=int, default=30)
     a = ap.parse_args()
     for layout in ("chunk", "stride"):  # reduce.hip reduce_chunked vs reduce_1pass
-        for blocks in (1024, 2048, 4096, 8192, 16384):
+        for blocks in (256, 512, 768, 1024, 1536, 2048, 4096):
             run("square_sum", {"BK_REDUCE_BLOCKS": str(blocks), "BK_REDUCE_LAYOUT": layout}, a.n, a.reps)
     run("philox_store", {}, a.n, a.reps)
     run("torch_sum", {}, a.n, a.reps)   # torch's own reduction over the same 800 MB (read roofline reference)
