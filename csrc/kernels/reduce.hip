@@ -39,11 +39,13 @@ constexpr int kRedBlock = 256;
 // (the workspace holds kRedMaxBlocks partials; the default grid is
 // kRedBlocks, BK_REDUCE_BLOCKS overrides it up to the workspace for sweeps)
 constexpr int kRedMaxBlocks = 32768;
-// 1024 blocks (4 per CU) with the block-contiguous layout: tools/reduce_sweep.py
-// on MI355X, 1e8 f64 square-sum, median of 30: 153 / 157 / 157 / 177 / 265 us
-// at 1024 / 2048 / 4096 / 8192 / 16384 blocks (the grid-stride layout 161 /
-// 170 / 174 / 178 / 249; profiles/r4_reduce_sweep.jsonl)
-constexpr int kRedBlocks = 1024;
+// 512 blocks (2 per CU, 8 waves, 16 x 16-B loads in flight per lane):
+// tools/reduce_sweep.py on MI355X, 1e8 f64 square-sum, median of 20 --
+// grid-stride layout 167 / 135 / 141 / 154 / 164 / 178 us at 256 / 512 / 768 /
+// 1024 / 2048 / 4096 blocks, block-contiguous 168 / 142 / 145 / 145 / 157 /
+// 158; torch.sum over the same 800 MB 139 us (profiles/r4_reduce_sweep*.jsonl;
+// the old 8192-block grid: 175-178 us)
+constexpr int kRedBlocks = 512;
 constexpr int kRedUnroll = 16;
 // the fused RNG->reduce kernels are compute-bound: 4 blocks per CU
 constexpr int kRandRedMaxBlocks = 1024;
@@ -238,8 +240,9 @@ __global__ __launch_bounds__(kRedBlock) void reduce_1pass(const T* __restrict__ 
 // layout above puts a lane's 16 loads gridDim x 4 KiB apart (32 MiB at 8192
 // blocks) -- every wave of the chip then hits the same few power-of-two
 // address strides at once (a channel-camping pattern); here the concurrent
-// reads are spread over the whole array.  BK_REDUCE_LAYOUT=stride keeps the
-// grid-stride kernel (A/B: tools/reduce_sweep.py).
+// reads are spread over the whole array.  Opt-in (BK_REDUCE_LAYOUT=chunk):
+// at the 512-block grid the grid-stride kernel measured faster
+// (tools/reduce_sweep.py, kRedBlocks).
 template <typename T, int OP, bool NT>
 __global__ __launch_bounds__(kRedBlock) void reduce_chunked(const T* __restrict__ a, const T* __restrict__ b,
                                                            int64_t n, double* __restrict__ partials,
@@ -366,7 +369,7 @@ int launch_reduce(const void* a, const void* b, int64_t n, double* workspace, do
   unsigned g = stream_grid(lanes_needed > 0 ? lanes_needed : 1, kRedBlock, (int)(red_blocks / kNumCU));
   if (g > (unsigned)red_blocks) g = (unsigned)red_blocks;  // the workspace holds kRedMaxBlocks partials
   unsigned* ticket = reinterpret_cast<unsigned*>(workspace + kRedMaxBlocks);
-  static const bool chunked = !(getenv("BK_REDUCE_LAYOUT") && !strcmp(getenv("BK_REDUCE_LAYOUT"), "stride"));
+  static const bool chunked = getenv("BK_REDUCE_LAYOUT") && !strcmp(getenv("BK_REDUCE_LAYOUT"), "chunk");
   const bool nt = stream_nt(n * (int64_t)sizeof(T) * (kTwoOperands<OP> ? 2 : 1));
   if (chunked) {
     if (nt) reduce_chunked<T, OP, true><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);

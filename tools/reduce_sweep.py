@@ -70,9 +70,10 @@ def main():
     ap.add_argument("--n", type=int, default=10**8)
     ap.add_argument("--reps", type=int, default=30)
     a = ap.parse_args()
-    for layout in ("chunk", "stride"):  # reduce.hip reduce_chunked vs reduce_1pass
-        for blocks in (256, 512, 768, 1024, 1536, 2048, 4096):
-            run("square_sum", {"BK_REDUCE_BLOCKS": str(blocks), "BK_REDUCE_LAYOUT": layout}, a.n, a.reps)
+    for _ in range(2):  # interleaved repeats: box-to-box and run-to-run noise is a few %
+        for layout in ("stride", "chunk"):  # reduce.hip reduce_1pass vs reduce_chunked
+            for blocks in (384, 512, 640, 768, 1024):
+                run("square_sum", {"BK_REDUCE_BLOCKS": str(blocks), "BK_REDUCE_LAYOUT": layout}, a.n, a.reps)
     run("philox_store", {}, a.n, a.reps)
     run("torch_sum", {}, a.n, a.reps)   # torch's own reduction over the same 800 MB (read roofline reference)
     run("d2d_copy", {}, a.n, a.reps)    # hipMemcpy device-to-device: 800 MB read + 800 MB written  # (its grid is fixed: kDrawBlocksPerCU, profiles/archive/r3_philox_grid_sweep.log)
