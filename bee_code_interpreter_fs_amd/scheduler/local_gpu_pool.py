@@ -345,7 +345,11 @@ class LocalGpuPoolBackend(CodeExecutor):
                     and st.get("ready_min", 0) >= st.get("min_target", 0)
                     and st.get("ready_min_cpu", 0) >= st.get("min_cpu_target", 0)
                     and st.get("ready_nano", 0) >= st.get("nano_target", 0)
-                    and st.get("ready_nano_cpu", 0) >= st.get("nano_cpu_target", 0))
+                    and st.get("ready_nano_cpu", 0) >= st.get("nano_cpu_target", 0)
+                    # warm gang rank sets (their HIP + torch init is seconds of
+                    # CPU per rank: done before READY, not inside the first
+                    # requests' window)
+                    and all(v == "ready" for v in (st.get("gang_warm") or {}).values()))
 
         while loop.time() < deadline:
             try:
