@@ -334,6 +334,10 @@ PyObject* py_apply(PyObject*, PyObject* args) {
       if (!seq) return nullptr;
       for (Py_ssize_t i = 0; i < PySequence_Fast_GET_SIZE(seq); ++i) {
         const long port = PyLong_AsLong(PySequence_Fast_GET_ITEM(seq, i));
+        if (port == -1 && PyErr_Occurred()) {
+          Py_DECREF(seq);
+          return nullptr;
+        }
         if (port >= 0 && port < 65536) connect_ports.push_back(port);
       }
       Py_DECREF(seq);
