@@ -184,6 +184,30 @@ def cpu_usage_s():
     return (sum(v) - v[3] - v[4]) / os.sysconf("SC_CLK_TCK"), "procstat"
 
 
+def cpu_throttle() -> dict:
+    """The container's CFS bandwidth counters (cgroup v2 cpu.stat or v1
+    cpu/cpu.stat): enforcement periods, periods in which the quota ran out,
+    and the time processes sat throttled -- {} without a quota."""
+    for path, scale in (("/sys/fs/cgroup/cpu.stat", 1.0), ("/sys/fs/cgroup/cpu/cpu.stat", 1e-3)):
+        try:
+            with open(path) as f:
+                kv = dict(line.split() for line in f if len(line.split()) == 2)
+        except OSError:
+            continue
+        if "nr_periods" in kv:
+            t = kv.get("throttled_usec") if scale == 1.0 else kv.get("throttled_time")
+            return {"periods": int(kv["nr_periods"]), "throttled": int(kv.get("nr_throttled", 0)),
+                    "throttled_ms": int(t or 0) * scale / 1e3}
+    return {}
+
+
+def throttle_delta(a: dict, b: dict):
+    if not a or not b:
+        return None
+    return {"periods": b["periods"] - a["periods"], "throttled_periods": b["throttled"] - a["throttled"],
+            "throttled_ms": round(b["throttled_ms"] - a["throttled_ms"], 1)}
+
+
 def _proc_times(pid: int):
     """(own CPU s, reaped children's CPU s) of a process, from /proc/<pid>/stat."""
     with open(f"/proc/{pid}/stat") as f:
@@ -573,7 +597,7 @@ def run_loadgens(n_procs, targets, source, concurrency, warmup, steps, sync, mar
     except Exception:
         pass
     if marks is not None:
-        marks["t0"], marks["cpu0"] = time.perf_counter(), cpu_usage_s()[0]
+        marks["t0"], marks["cpu0"], marks["thr0"] = time.perf_counter(), cpu_usage_s()[0], cpu_throttle()
         marks["roles0"] = cpu_by_role(marks.get("svc"))
         marks["threads0"] = daemon_threads(marks.get("svc"))
         if marks.get("hport"):
@@ -854,6 +878,7 @@ def main():
                                                  marks, first=first, extra=extra))
             elapsed = max(g[0] for g in gathered)
             cpu_busy = (cpu_usage_s()[0] - marks["cpu0"]) / max(time.perf_counter() - marks["t0"], 1e-9)
+            thr0, thr1 = marks.get("thr0") or {}, cpu_throttle()
             roles0, roles1 = marks["roles0"], marks.get("roles1")
             slots0, slots1 = marks.get("slots0"), marks.get("slots1")
             threads0, threads1 = marks.get("threads0"), marks.get("threads1")
@@ -862,6 +887,7 @@ def main():
             loop.run_until_complete(run_clients(stubs, source, args.warmup, extra=extra))  # warm every pool
             barrier()
             cpu0, cpu_src = cpu_usage_s()
+            thr0 = cpu_throttle()
             roles0 = cpu_by_role(svc_pid)
             threads0 = daemon_threads(svc_pid)
             slots0 = slot_executions(hport) if rank == 0 else None
@@ -871,6 +897,7 @@ def main():
                 run_clients(stubs, source, args.steps, trace, extra=extra))
             barrier()
             elapsed = time.perf_counter() - t0
+            thr1 = cpu_throttle()
             roles1 = cpu_by_role(svc_pid)
             threads1 = daemon_threads(svc_pid)
             slots1 = slot_executions(hport) if rank == 0 else None
@@ -1008,6 +1035,12 @@ def main():
             quota, quota_src = cpu_quota_cores()
             bound = {"cpu_quota_cores": round(quota, 2), "quota_source": quota_src,
                      "cpu_utilisation_of_quota": round(cpu_busy / quota, 3) if quota else None}
+            # quota enforcement during the timed window: periods in which the
+            # container ran out of quota stall every process of it until the
+            # next period (latency the GPU never sees)
+            thr = throttle_delta(thr0, thr1)
+            if thr is not None:
+                bound["cpu_throttling"] = thr
             if "cpu_ms_per_exec" in out and out["cpu_ms_per_exec"]["all_cgroup"] > 0:
                 cap = quota * 1e3 / out["cpu_ms_per_exec"]["all_cgroup"]
                 bound["cpu_bound_rps"] = round(cap, 1)
