@@ -133,6 +133,19 @@ enum : int {
   // panel's buffer descriptor once per K-tile, every load's SGPR offset is
   // loop-invariant (one SALU fewer per load; hipBLASLt's form)
   kConstSoff = 4194304,
+  // kAsmMfma|kInterleave, two barriers per K-tile (ktile_asm2): the wait for
+  // the next K-tile's loads in the middle of the second k-half
+  kTwoBar = 8388608,
+  // kTwoBar: the K-tile wait at group 10 / 12 of the second k-half (default 8)
+  kTwoBarG10 = 16777216,
+  kTwoBarG12 = 33554432,
+  // the LDS-staged epilogue's 16-B stores non-temporal (hipBLASLt's "NTD")
+  kNtStore = 67108864,
+  // DIAGNOSTICS of kTwoBar (lab only, racy C): drop the K-tile vmcnt wait,
+  // the second barrier, or the first lgkmcnt(0) + barrier -- what each costs
+  kDiagNoVmWait = 134217728,
+  kDiagNoBar2 = 268435456,
+  kDiagNoBar1 = 536870912,
 };
 // (the stamps' running total while a kDiagStamps kernel runs: one per wave)
 struct StampAcc {
@@ -660,7 +673,120 @@ __device__ __forceinline__ void ktile_asm3(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8],
   }
 }
 
-template <bool OUT_BF16>
+// One K-tile with two barriers (kTwoBar): the K-tile wait moves from the
+// k-half boundary to the middle of the second k-half.  32 groups of 4 MFMAs
+// fenced by sched_barrier(0), as ktile_asm's kSpacedMem form:
+//   k-half 0, g 0-7    2 ds_read of the k-half-1 fragments (cur) per group,
+//                      between the MFMA pairs: all 16 issued by MFMA 32, so
+//                      the lgkmcnt(0) below has 32 MFMAs to cover them
+//   end of k-half 0    s_waitcnt lgkmcnt(0); s_barrier   -> cur is free
+//   k-half 1, g 0-7    one glds of tile t+2 -> cur per group (A)
+//   k-half 1, g 8      s_waitcnt vmcnt(8); s_barrier     -> tile t+1 (the glds
+//                      one iteration earlier) landed for every wave; only this
+//                      iteration's 8 younger glds may still be in flight
+//   k-half 1, g 8-15   one glds (B) + 2 ds_read of tile t+1's k-half-0
+//                      fragments (nxt) per group, in the order the next
+//                      K-tile consumes them
+// Why: PMC at 8192^3 (profiles/r4_gemm_pmc.md) put the gap to hipBLASLt in
+// SQ_WAIT_ANY -- 423 vs 105 cycles per wave per K-tile at equal
+// SQ_WAIT_INST_ANY -- and the one-barrier loop gave a K-tile load only
+// 68-128 MFMAs to land; here it has 100-160.  WAR: the earliest k-half-1
+// fragment write lands >= 20 MFMAs after its last reader (fa1[i] first, then
+// fb1[0..3], fa1[6], fb1[4..7], fa1[7]: each after its last use + 16).
+template <bool INIT, bool KT = false, bool NN = false, int WG = 8, int DIAG = 0>
+__device__ __forceinline__ void ktile_asm2(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8], bf16x8 (&fa1)[8],
+                                           bf16x8 (&fb1)[8], uint16_t* smem, const Panel& pa, const Panel& pb, int t,
+                                           int nk, int wr, int wc, int lane, int wave) {
+  uint16_t* cur = smem + (t & 1) * kBuf;
+  uint16_t* nxt = smem + ((t & 1) ^ 1) * kBuf;
+  const int rl = lane & 15, ch = lane >> 4;
+  // k-half-1 fragment j of the 16 in WAR-safe order (see above): 0-5 fa1[0..5],
+  // 6-9 fb1[0..3], 10 fa1[6], 11-14 fb1[4..7], 15 fa1[7]
+  auto read1 = [&](int j) {
+    if (j < 6) fa1[j] = frag(cur, wr * 128 + j * 16 + rl, 4 + ch);
+    else if (j < 10) fb1[j - 6] = fragB(cur + kOperand, wc, j - 6, 1, lane, NN);
+    else if (j == 10) fa1[6] = frag(cur, wr * 128 + 6 * 16 + rl, 4 + ch);
+    else if (j < 15) fb1[j - 7] = fragB(cur + kOperand, wc, j - 7, 1, lane, NN);
+    else fa1[7] = frag(cur, wr * 128 + 7 * 16 + rl, 4 + ch);
+  };
+  // tile t+1's k-half-0 fragment i, in consumption order: fa0[0], fb0[0..7], fa0[1..7]
+  auto read0 = [&](int i) {
+    if (i == 0) fa0[0] = frag(nxt, wr * 128 + rl, ch);
+    else if (i <= 8) fb0[i - 1] = fragB(nxt + kOperand, wc, i - 1, 0, lane, NN);
+    else fa0[i - 8] = frag(nxt, wr * 128 + (i - 8) * 16 + rl, ch);
+  };
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    auto m0 = [&](int jj) { mfma_ab<INIT, false>(acc[g >> 1][(g & 1) * 4 + jj], fa0[g >> 1], fb0[(g & 1) * 4 + jj]); };
+    m0(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (g < 8) read1(2 * g);
+    __builtin_amdgcn_sched_barrier(0);
+    m0(1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (g < 8) read1(2 * g + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    m0(2);
+    m0(3);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr ((DIAG & kDiagNoBar1) == 0) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier();
+  }
+  const int kn = min(t + 2, nk - 1) * TK;
+  static_assert(WG == 8 || WG == 10 || WG == 12, "kTwoBar wait group");
+  // tile t+1's 16 fragment reads over groups WG..15: read i in group
+  // WG + i * (16 - WG) / 16, up to 4 per group, one after each of MFMA 1-3
+  // (and a 4th after the last)
+  constexpr int kSpan = 16 - WG;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    auto m1 = [&](int jj) { mfma_ab<false, false>(acc[g >> 1][(g & 1) * 4 + jj], fa1[g >> 1], fb1[(g & 1) * 4 + jj]); };
+    if (g == WG) {
+      // tile t+1 landed: only this iteration's WG younger glds may be in flight
+      if constexpr ((DIAG & kDiagNoVmWait) != 0) {
+      } else if constexpr (WG == 8) {
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else if constexpr (WG == 10) {
+        asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      }
+      if constexpr ((DIAG & kDiagNoBar2) == 0) barrier();
+    }
+    m1(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (g < 8) {
+      if constexpr (NN) glds_a_raw(pa, kn, cur, wave, g);
+      else glds_one(pa, kn, cur, wave, g, KT);
+    } else if constexpr (NN) {
+      glds_nn(pb, kn, cur + kOperand, wave, g - 8);
+    } else {
+      glds_one(pb, kn, cur + kOperand, wave, g - 8, KT);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // the reads of this group: i with WG + i * kSpan / 16 == g
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (g >= WG && WG + i * kSpan / 16 == g) {
+        if (k < 3) m1(1 + k);  // (a 4th read of the group follows the 4th MFMA)
+        __builtin_amdgcn_sched_barrier(0);
+        read0(i);
+        __builtin_amdgcn_sched_barrier(0);
+        ++k;
+      }
+    }
+#pragma unroll
+    for (int jj = 1; jj < 4; ++jj)
+      if (jj > k) m1(jj);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <bool OUT_BF16, bool NT = false>
 __device__ __forceinline__ void epilogue(uint16_t* smem, const f32x4 (&acc)[8][8], void* __restrict__ C, int ldc,
                                          int64_t row0, int col0, int wave, int lane, float alpha, float beta) {
   float* ep = reinterpret_cast<float*>(smem) + wave * kEpWaveFloats;
@@ -696,7 +822,13 @@ __device__ __forceinline__ void epilogue(uint16_t* smem, const f32x4 (&acc)[8][8
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           packed[e] = (uint32_t)float_to_bf16_bits(v[2 * e]) | ((uint32_t)float_to_bf16_bits(v[2 * e + 1]) << 16);
-        *dst = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+        if constexpr (NT) {
+          typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+          const u32x4 pk = {packed[0], packed[1], packed[2], packed[3]};
+          __builtin_nontemporal_store(pk, reinterpret_cast<u32x4*>(dst));
+        } else {
+          *dst = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+        }
       }
     } else {
       // 32 lanes x 4 columns per row, 2 rows per pass
@@ -706,7 +838,8 @@ __device__ __forceinline__ void epilogue(uint16_t* smem, const f32x4 (&acc)[8][8
         f32x4 v = *reinterpret_cast<const f32x4*>(ep + row * kEpPitch + col);
         f32x4* dst = reinterpret_cast<f32x4*>((float*)C + (grow0 + row) * ldc + col0 + col);
         if (beta != 0.f) v += beta * *dst;
-        *dst = v;
+        if constexpr (NT) __builtin_nontemporal_store(v, dst);
+        else *dst = v;
       }
     }
   }
@@ -881,6 +1014,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
     ktile_asm3<true, edge, nn, spread>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
     for (int t = 1; t < nk; ++t)
       ktile_asm3<false, edge, nn, spread>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
+  } else if constexpr (am && inter && (O & kTwoBar) != 0) {
+    static_assert(!sw, "kTwoBar: B fragments in the plain layout");
+    constexpr int wg = (O & kTwoBarG10) ? 10 : (O & kTwoBarG12) ? 12 : 8;
+    constexpr int diag = O & (kDiagNoVmWait | kDiagNoBar2 | kDiagNoBar1);
+    read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn);
+    ktile_asm2<true, edge, nn, wg, diag>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
+    for (int t = 1; t < nk; ++t)
+      ktile_asm2<false, edge, nn, wg, diag>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
   } else if constexpr (am && inter && (O & kAltSimd) != 0) {
     read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn, sw);
     // HW_ID bit 4 = the SIMD's parity (s_getreg_b32 hwreg(HW_REG_HW_ID, 4, 1))
@@ -1014,7 +1155,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
                       ((uintptr_t)C & 15) != 0)) {
     epilogue_masked<OUT_BF16>(smem, acc, C, ldc, m0 + wr * 128, n0 + wc * 128, M, N, wave, lane, alpha, beta);
   } else {
-    epilogue<OUT_BF16>(smem, acc, C, ldc, m0 + wr * 128, n0 + wc * 128, wave, lane, alpha, beta);
+    epilogue<OUT_BF16, (O & kNtStore) != 0>(smem, acc, C, ldc, m0 + wr * 128, n0 + wc * 128, wave, lane, alpha, beta);
   }
 }
 

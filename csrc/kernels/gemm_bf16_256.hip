@@ -12,11 +12,15 @@
 namespace bk {
 
 constexpr int kShipped = g256::kOptRound1;
-// kSpacedMem: each group's LDS-DMA load and LDS read pinned apart between its
-// MFMAs (M G M M r M); s_memtime stamps: the second k-half 1366-1384 vs
-// 1408-1427 cycles per K-tile, 1417 vs 1373 TFLOP/s at 4096^3
-// (profiles/r3_gemm_lab_spaced.log)
-constexpr int kShippedW4 = g4::kAsmMfma | g4::kInterleave | g4::kSpacedMem;
+// kTwoBar | kTwoBarG10: the wait for the next K-tile's loads moved from the
+// k-half boundary to group 10 of the second k-half (loads get 100-160 MFMAs
+// to land instead of 68-128: SQ_WAIT_ANY 407 -> 281 cycles per wave per
+// K-tile at 8192^3); kNtStore: non-temporal C stores, as hipBLASLt's NTD
+// kernels.  Interleaved A/B on one MI355X (profiles/r4_gemm_pmc.md,
+// tools/gemm_lab.py): 4096^3 98.9 -> 94.5 us (hipBLASLt 93.6), 8192^3
+// 739 -> 705 us (hipBLASLt 671).  Before: kSpacedMem (M G M M r M groups,
+// profiles/r3_gemm_lab_spaced.log).
+constexpr int kShippedW4 = g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore;
 constexpr int kW4MinK = 256;
 
 bool gemm256_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16) {

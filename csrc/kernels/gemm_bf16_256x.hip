@@ -7,6 +7,11 @@
 namespace bk {
 
 constexpr int kShippedW4x = g4::kAsmMfma | g4::kInterleave;
+// the edge kernel runs the aligned kernel's two-barrier schedule and
+// non-temporal stores (gemm_bf16_256.hip kShippedW4; tools/gemm_lab.py
+// w4_asm_twobar_ntstore_edge).  (The [K][N] kernel keeps its schedule: with
+// kNtStore its f32-output instance spills 4 VGPRs.)
+constexpr int kShippedW4Edge = kShippedW4x | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore;
 
 // the 4-wave 256x256 kernel on any M x N (K a multiple of 64): ragged
 // borders read zeros and store under a mask (g4::kEdge)
@@ -14,7 +19,7 @@ bool gemm256_edge_ok(int M, int N, int K, int lda, int ldb) { return g4::edge_ok
 
 void launch_gemm256_edge(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                          float alpha, float beta, bool out_bf16, hipStream_t stream) {
-  g4::launch<kShippedW4x | g4::kEdge>(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, out_bf16, stream);
+  g4::launch<kShippedW4Edge | g4::kEdge>(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, out_bf16, stream);
 }
 
 // C = A . B with B stored [K][N] (no transpose pass): the 4-wave kernel with

@@ -31,8 +31,11 @@ NAMES = {0: "round1", 1: "keep_b0", 2: "round1_nostagger", 3: "keep_b0_nostagger
          29: "w4_asm_altsimd", 30: "w4_asm_altsimd_swapab", 31: "w4_asm_altsimd_early", 32: "diag_w4_asm_stamps", 33: "diag_w4_asm_stamps_noglds",
          34: "diag_w4_asm_stamps_split", 35: "w4_asm_splitglds", 36: "diag_w4_asm_noglds",
          37: "w4_asm_spaced", 38: "diag_w4_asm_stamps_spaced", 39: "w4_asm_spaced_edge", 40: "diag_w4_asm_stamps_mfma_only",
-         41: "w4_asm_spaced_csoff", 42: "diag_w4_asm_stamps_spaced_csoff"}
-DIAG = {4, 5, 25, 28, 32, 33, 34, 36, 38, 40, 42}
+         41: "w4_asm_spaced_csoff", 42: "diag_w4_asm_stamps_spaced_csoff", 43: "w4_asm_twobar", 44: "w4_asm_twobar_edge",
+         45: "w4_asm_twobar_g10", 46: "w4_asm_twobar_g12", 47: "w4_asm_spaced_ntstore", 48: "w4_asm_twobar_ntstore",
+         49: "w4_asm_twobar_g10_ntstore", 50: "w4_asm_twobar_ntstore_edge",
+         51: "diag_twobar_no_vmwait", 52: "diag_twobar_no_bar2", 53: "diag_twobar_no_bar1", 54: "diag_twobar_no_syncs"}
+DIAG = {4, 5, 25, 28, 32, 33, 34, 36, 38, 40, 42, 51, 52, 53, 54}
 PROD = None
 
 
@@ -109,7 +112,8 @@ def main():
     p.add_argument("--variants", type=int, nargs="*", default=None)
     p.add_argument("--no-check", action="store_true")
     p.add_argument("--stamps", action="store_true", help="kDiagStamps: cycles per K-tile and in its wait + barrier")
-    p.add_argument("--one", type=int, default=None, help="only run this variant (-1 = hipBLASLt) --reps times at 4096^3 (rocprofv3 passes)")
+    p.add_argument("--one", type=int, default=None, help="only run this variant (-1 = hipBLASLt) --reps times at --size^3 (rocprofv3 passes)")
+    p.add_argument("--size", type=int, default=4096, help="--one: M = N = K")
     args = p.parse_args()
     torch.cuda.init()
     lib = load()
@@ -143,9 +147,10 @@ def main():
                               "half1_cycles_per_ktile_median": float(statistics.median(h1 / nk))}), flush=True)
         return
     if args.one is not None:
-        a = torch.empty(4096, 4096, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
-        bt = torch.empty(4096, 4096, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
-        c = torch.empty(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        n = args.size
+        a = torch.empty(n, n, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
+        bt = torch.empty(n, n, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
+        c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
         for _ in range(args.reps):
             run(lib, args.one, a, bt, c) if args.one >= 0 else torch.matmul(a, bt.T, out=c)
         torch.cuda.synchronize()

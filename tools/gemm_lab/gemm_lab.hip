@@ -54,7 +54,20 @@ constexpr int kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave, g4::kNoCarry, g4::
                            g4::kAsmMfma | g4::kInterleave | g4::kSpacedMem | g4::kEdge,
                            g4::kAsmMfma | g4::kInterleave | g4::kDiagStamps | g4::kDiagMfmaOnly,
                            g4::kAsmMfma | g4::kInterleave | g4::kSpacedMem | g4::kConstSoff,
-                           g4::kAsmMfma | g4::kInterleave | g4::kDiagStamps | g4::kSpacedMem | g4::kConstSoff};
+                           g4::kAsmMfma | g4::kInterleave | g4::kDiagStamps | g4::kSpacedMem | g4::kConstSoff,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kEdge,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG12,
+                           g4::kAsmMfma | g4::kInterleave | g4::kSpacedMem | g4::kNtStore,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kNtStore,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kNtStore | g4::kEdge,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore | g4::kDiagNoVmWait,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore | g4::kDiagNoBar2,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore | g4::kDiagNoBar1,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore |
+                               g4::kDiagNoVmWait | g4::kDiagNoBar2 | g4::kDiagNoBar1};
 template <int I>
 void run_w4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool bf,
             hipStream_t s) {
@@ -111,6 +124,18 @@ BK_API int gemmlab_run(int variant, const void* A, const void* Bt, void* C, int 
     case 40: run_w4<34>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 41: run_w4<35>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 42: run_w4<36>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 43: run_w4<37>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 44: run_w4<38>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 45: run_w4<39>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 46: run_w4<40>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 47: run_w4<41>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 48: run_w4<42>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 49: run_w4<43>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 50: run_w4<44>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 51: run_w4<45>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 52: run_w4<46>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 53: run_w4<47>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 54: run_w4<48>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     default: return kBadArgument;
   }
   return launch_status();
