@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import gc
 import json
 import math
 import os
@@ -555,6 +556,9 @@ def _loadgen_main(targets, first, source, concurrency, warmup, steps, barrier, r
     try:
         chans, stubs = loop.run_until_complete(open_clients(targets, first, concurrency))
         loop.run_until_complete(run_clients(stubs, source, warmup, extra=extra))
+        if os.environ.get("BEE_GC_FREEZE", "1") != "0":
+            gc.collect()
+            gc.freeze()  # this load generator's heap out of the timed window's collections
         barrier.wait()
         if go is not None:
             go.wait()
@@ -885,6 +889,9 @@ def main():
         else:
             chans, stubs = loop.run_until_complete(open_clients(targets, first, args.concurrency))
             loop.run_until_complete(run_clients(stubs, source, args.warmup, extra=extra))  # warm every pool
+            if os.environ.get("BEE_GC_FREEZE", "1") != "0":
+                gc.collect()
+                gc.freeze()  # the clients' heap out of the timed window's collections
             barrier()
             cpu0, cpu_src = cpu_usage_s()
             thr0 = cpu_throttle()
