@@ -146,6 +146,9 @@ enum : int {
   kDiagNoVmWait = 134217728,
   kDiagNoBar2 = 268435456,
   kDiagNoBar1 = 536870912,
+  // DIAGNOSTIC of kTwoBar (wrong C): skip the next K-tile's fragment reads
+  // (the k-half-0 MFMAs reuse stale fragments); with kDiagNoGlds: no K-loop loads
+  kDiagNoReads0 = 1073741824,
 };
 // (the stamps' running total while a kDiagStamps kernel runs: one per wave)
 struct StampAcc {
@@ -758,7 +761,8 @@ __device__ __forceinline__ void ktile_asm2(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8],
     }
     m1(0);
     __builtin_amdgcn_sched_barrier(0);
-    if (g < 8) {
+    if constexpr ((DIAG & kDiagNoGlds) != 0) {
+    } else if (g < 8) {
       if constexpr (NN) glds_a_raw(pa, kn, cur, wave, g);
       else glds_one(pa, kn, cur, wave, g, KT);
     } else if constexpr (NN) {
@@ -774,7 +778,7 @@ __device__ __forceinline__ void ktile_asm2(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8],
       if (g >= WG && WG + i * kSpan / 16 == g) {
         if (k < 3) m1(1 + k);  // (a 4th read of the group follows the 4th MFMA)
         __builtin_amdgcn_sched_barrier(0);
-        read0(i);
+        if constexpr ((DIAG & kDiagNoReads0) == 0) read0(i);
         __builtin_amdgcn_sched_barrier(0);
         ++k;
       }
@@ -1017,7 +1021,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   } else if constexpr (am && inter && (O & kTwoBar) != 0) {
     static_assert(!sw, "kTwoBar: B fragments in the plain layout");
     constexpr int wg = (O & kTwoBarG10) ? 10 : (O & kTwoBarG12) ? 12 : 8;
-    constexpr int diag = O & (kDiagNoVmWait | kDiagNoBar2 | kDiagNoBar1);
+    constexpr int diag = O & (kDiagNoVmWait | kDiagNoBar2 | kDiagNoBar1 | kDiagNoReads0 | kDiagNoGlds);
     read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn);
     ktile_asm2<true, edge, nn, wg, diag>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
     for (int t = 1; t < nk; ++t)
