@@ -696,7 +696,7 @@ __device__ __forceinline__ void ktile_asm3(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8],
 // 68-128 MFMAs to land; here it has 100-160.  WAR: the earliest k-half-1
 // fragment write lands >= 20 MFMAs after its last reader (fa1[i] first, then
 // fb1[0..3], fa1[6], fb1[4..7], fa1[7]: each after its last use + 16).
-template <bool INIT, bool KT = false, bool NN = false, int WG = 8, int DIAG = 0>
+template <bool INIT, bool KT = false, bool NN = false, int WG = 8, int DIAG = 0, bool SW = false>
 __device__ __forceinline__ void ktile_asm2(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8], bf16x8 (&fa1)[8],
                                            bf16x8 (&fb1)[8], uint16_t* smem, const Panel& pa, const Panel& pb, int t,
                                            int nk, int wr, int wc, int lane, int wave) {
@@ -707,21 +707,21 @@ __device__ __forceinline__ void ktile_asm2(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8],
   // 6-9 fb1[0..3], 10 fa1[6], 11-14 fb1[4..7], 15 fa1[7]
   auto read1 = [&](int j) {
     if (j < 6) fa1[j] = frag(cur, wr * 128 + j * 16 + rl, 4 + ch);
-    else if (j < 10) fb1[j - 6] = fragB(cur + kOperand, wc, j - 6, 1, lane, NN);
+    else if (j < 10) fb1[j - 6] = fragB(cur + kOperand, wc, j - 6, 1, lane, NN, SW);
     else if (j == 10) fa1[6] = frag(cur, wr * 128 + 6 * 16 + rl, 4 + ch);
-    else if (j < 15) fb1[j - 7] = fragB(cur + kOperand, wc, j - 7, 1, lane, NN);
+    else if (j < 15) fb1[j - 7] = fragB(cur + kOperand, wc, j - 7, 1, lane, NN, SW);
     else fa1[7] = frag(cur, wr * 128 + 7 * 16 + rl, 4 + ch);
   };
   // tile t+1's k-half-0 fragment i, in consumption order: fa0[0], fb0[0..7], fa0[1..7]
   auto read0 = [&](int i) {
     if (i == 0) fa0[0] = frag(nxt, wr * 128 + rl, ch);
-    else if (i <= 8) fb0[i - 1] = fragB(nxt + kOperand, wc, i - 1, 0, lane, NN);
+    else if (i <= 8) fb0[i - 1] = fragB(nxt + kOperand, wc, i - 1, 0, lane, NN, SW);
     else fa0[i - 8] = frag(nxt, wr * 128 + (i - 8) * 16 + rl, ch);
   };
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
-    auto m0 = [&](int jj) { mfma_ab<INIT, false>(acc[g >> 1][(g & 1) * 4 + jj], fa0[g >> 1], fb0[(g & 1) * 4 + jj]); };
+    auto m0 = [&](int jj) { mfma_ab<INIT, SW>(acc[g >> 1][(g & 1) * 4 + jj], fa0[g >> 1], fb0[(g & 1) * 4 + jj]); };
     m0(0);
     __builtin_amdgcn_sched_barrier(0);
     if (g < 8) read1(2 * g);
@@ -746,7 +746,7 @@ __device__ __forceinline__ void ktile_asm2(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8],
   constexpr int kSpan = 16 - WG;
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
-    auto m1 = [&](int jj) { mfma_ab<false, false>(acc[g >> 1][(g & 1) * 4 + jj], fa1[g >> 1], fb1[(g & 1) * 4 + jj]); };
+    auto m1 = [&](int jj) { mfma_ab<false, SW>(acc[g >> 1][(g & 1) * 4 + jj], fa1[g >> 1], fb1[(g & 1) * 4 + jj]); };
     if (g == WG) {
       // tile t+1 landed: only this iteration's WG younger glds may be in flight
       if constexpr ((DIAG & kDiagNoVmWait) != 0) {
@@ -971,7 +971,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
   constexpr bool edge = (O & kEdge) != 0, nn = (O & kNN) != 0, sw = (O & kSwapAB) != 0;
   static_assert(!(edge && nn), "kNN is for tile-multiple shapes");
   static_assert(!(sw && nn), "kSwapAB permutes B's rows: TN only");
-  static_assert(!sw || (am && inter && (O & kThreeBar) == 0), "kSwapAB: the ktile_asm schedule");
+  static_assert(!sw || (am && inter && (O & kThreeBar) == 0), "kSwapAB: the ktile_asm / ktile_asm2 schedules");
   const int nbm = edge ? (M + TM - 1) / TM : M / TM, nbn = edge ? (N + TN - 1) / TN : N / TN, nblocks = nbm * nbn;
   const int b = xcd_remap(blockIdx.x, nblocks);
   constexpr int kGm = (O & kGroup2) ? 2 : (O & kGroup8) ? 8 : (O & kGroup16) ? 16 : kGroupM;
@@ -1019,13 +1019,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
     for (int t = 1; t < nk; ++t)
       ktile_asm3<false, edge, nn, spread>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
   } else if constexpr (am && inter && (O & kTwoBar) != 0) {
-    static_assert(!sw, "kTwoBar: B fragments in the plain layout");
     constexpr int wg = (O & kTwoBarG10) ? 10 : (O & kTwoBarG12) ? 12 : 8;
     constexpr int diag = O & (kDiagNoVmWait | kDiagNoBar2 | kDiagNoBar1 | kDiagNoReads0 | kDiagNoGlds);
-    read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn);
-    ktile_asm2<true, edge, nn, wg, diag>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
+    read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn, sw);
+    ktile_asm2<true, edge, nn, wg, diag, sw>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
     for (int t = 1; t < nk; ++t)
-      ktile_asm2<false, edge, nn, wg, diag>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
+      ktile_asm2<false, edge, nn, wg, diag, sw>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
   } else if constexpr (am && inter && (O & kAltSimd) != 0) {
     read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn, sw);
     // HW_ID bit 4 = the SIMD's parity (s_getreg_b32 hwreg(HW_REG_HW_ID, 4, 1))
