@@ -98,3 +98,50 @@ def test_headline_checks_bite():
     bad[256:512, 1024:1280] = 0.0                        # one corrupt tile
     err_bad = np.abs(bad.sum(axis=1, dtype=np.float64) - ref).max()
     assert not bench.gemm_row_ok(err_bad), err_bad
+
+
+def test_gang_check_is_bounded_and_stops_at_the_first_failure(monkeypatch):
+    """The gang check runs after the timed window on the driver's multi-GPU
+    node; a gang that fails (or hangs) must not eat the run: the first
+    failing run ends it, and one time budget bounds all of them."""
+    import importlib.util
+    import time
+    import types
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    calls = []
+
+    class Stub:
+        def __init__(self, ch):
+            pass
+
+        def Execute(self, req, timeout):  # noqa: N802 - the gRPC method name
+            calls.append((req.timeout, timeout))
+            return types.SimpleNamespace(exit_code=1, stdout="", stderr="rccl init failed", timings_ms={})
+
+    class Chan:
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+
+    import grpc
+
+    from bee_code_interpreter_fs_amd.models import proto as pb
+
+    monkeypatch.setattr(grpc, "insecure_channel", lambda target: Chan())
+    monkeypatch.setattr(pb, "CodeInterpreterServiceStub", Stub)
+    t = time.monotonic()
+    out = bench.gang_allreduce_check("127.0.0.1:1", 8, repeats=2, hport=None)
+    assert time.monotonic() - t < 5
+    assert len(calls) == 1 and not out["ok"], out  # no second try of a failing gang
+    assert out["runs"][0]["stderr_tail"].endswith("rccl init failed")
+    assert calls[0][0] <= 180 and calls[0][1] <= 240  # script and RPC bounded by the budget
+
+    calls.clear()
+    monkeypatch.setenv("BEE_BENCH_GANG_BUDGET_S", "10")
+    out = bench.gang_allreduce_check("127.0.0.1:1", 8, repeats=2, hport=None)
+    assert calls == [] and "budget" in out.get("skipped", ""), out
