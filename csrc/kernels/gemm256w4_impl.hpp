@@ -62,7 +62,7 @@ constexpr int kSmemBytes = 2 * kBuf * 2;  // 128 KiB (epilogue needs 66 KiB)
 static_assert(4 * kEpWaveFloats * 4 <= kSmemBytes, "epilogue staging fits");
 
 // options
-enum : int {
+enum : long long {
   kPinOrder = 1,    // sched_barrier fences around each MFMA block
   kInterleave = 2,  // sched_group_barrier: spread ds_read / glds among the MFMAs
   kNoCarry = 4,     // no fragment prefetch across the barrier: both k-halves read at the top of the iteration
@@ -149,6 +149,10 @@ enum : int {
   // DIAGNOSTIC of kTwoBar (wrong C): skip the next K-tile's fragment reads
   // (the k-half-0 MFMAs reuse stale fragments); with kDiagNoGlds: no K-loop loads
   kDiagNoReads0 = 1073741824,
+  // kTwoBar: the 16 k-half-1 fragment reads over groups 0-11 of the first
+  // k-half (2, 2, 2, 2, then 1 per group) instead of 0-7 (2 per group): a
+  // lighter LDS read burst next to the landing K-tile loads
+  kReads12 = 1LL << 31,
 };
 // (the stamps' running total while a kDiagStamps kernel runs: one per wave)
 struct StampAcc {
@@ -696,7 +700,7 @@ __device__ __forceinline__ void ktile_asm3(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8],
 // 68-128 MFMAs to land; here it has 100-160.  WAR: the earliest k-half-1
 // fragment write lands >= 20 MFMAs after its last reader (fa1[i] first, then
 // fb1[0..3], fa1[6], fb1[4..7], fa1[7]: each after its last use + 16).
-template <bool INIT, bool KT = false, bool NN = false, int WG = 8, int DIAG = 0, bool SW = false>
+template <bool INIT, bool KT = false, bool NN = false, int WG = 8, int DIAG = 0, bool SW = false, int RG = 8>
 __device__ __forceinline__ void ktile_asm2(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8], bf16x8 (&fa1)[8],
                                            bf16x8 (&fb1)[8], uint16_t* smem, const Panel& pa, const Panel& pb, int t,
                                            int nk, int wr, int wc, int lane, int wave) {
@@ -722,13 +726,18 @@ __device__ __forceinline__ void ktile_asm2(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8],
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
     auto m0 = [&](int jj) { mfma_ab<INIT, SW>(acc[g >> 1][(g & 1) * 4 + jj], fa0[g >> 1], fb0[(g & 1) * 4 + jj]); };
+    // RG = 8: reads 2g, 2g+1 in group g < 8; RG = 12: reads 2g, 2g+1 in
+    // groups 0-3, read g + 4 in groups 4-11 (the same order, so the same WAR
+    // distances or longer)
+    constexpr bool two = RG == 8 ? true : false;
     m0(0);
     __builtin_amdgcn_sched_barrier(0);
-    if (g < 8) read1(2 * g);
+    if (two ? g < 8 : g < 4) read1(2 * g);
+    else if (!two && g < 12) read1(g + 4);
     __builtin_amdgcn_sched_barrier(0);
     m0(1);
     __builtin_amdgcn_sched_barrier(0);
-    if (g < 8) read1(2 * g + 1);
+    if (two ? g < 8 : g < 4) read1(2 * g + 1);
     __builtin_amdgcn_sched_barrier(0);
     m0(2);
     m0(3);
@@ -959,7 +968,7 @@ __device__ __forceinline__ void epilogue_masked(uint16_t* smem, const f32x4 (&ac
   }
 }
 
-template <bool OUT_BF16, int O>
+template <bool OUT_BF16, long long O>
 __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t* __restrict__ A,
                                                                   const uint16_t* __restrict__ Bt,
                                                                   void* __restrict__ C, int M, int N, int K, int lda,
@@ -1020,11 +1029,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_tn_256w4(const uint16_t
       ktile_asm3<false, edge, nn, spread>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
   } else if constexpr (am && inter && (O & kTwoBar) != 0) {
     constexpr int wg = (O & kTwoBarG10) ? 10 : (O & kTwoBarG12) ? 12 : 8;
-    constexpr int diag = O & (kDiagNoVmWait | kDiagNoBar2 | kDiagNoBar1 | kDiagNoReads0 | kDiagNoGlds);
+    constexpr int diag = (int)(O & (kDiagNoVmWait | kDiagNoBar2 | kDiagNoBar1 | kDiagNoReads0 | kDiagNoGlds));
+    constexpr int rg = (O & kReads12) ? 12 : 8;
     read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn, sw);
-    ktile_asm2<true, edge, nn, wg, diag, sw>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
+    ktile_asm2<true, edge, nn, wg, diag, sw, rg>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, 0, nk, wr, wc, lane, wave);
     for (int t = 1; t < nk; ++t)
-      ktile_asm2<false, edge, nn, wg, diag, sw>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
+      ktile_asm2<false, edge, nn, wg, diag, sw, rg>(acc, fa0, fb0, fa1, fb1, smem, pa, pb, t, nk, wr, wc, lane, wave);
   } else if constexpr (am && inter && (O & kAltSimd) != 0) {
     read_frags(smem, wr, wc, lane, 0, fa0, fb0, nn, sw);
     // HW_ID bit 4 = the SIMD's parity (s_getreg_b32 hwreg(HW_REG_HW_ID, 4, 1))
@@ -1184,7 +1194,7 @@ inline bool edge_ok(int M, int N, int K, int lda, int ldb) {
   return M > 0 && N > 0 && K > 0 && K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && span_ok(lda) && span_ok(ldb);
 }
 
-template <int O>
+template <long long O>
 inline void launch(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
                    float beta, bool out_bf16, hipStream_t stream) {
   const unsigned grid = (O & kEdge) ? (unsigned)(((M + TM - 1) / TM) * ((N + TN - 1) / TN))

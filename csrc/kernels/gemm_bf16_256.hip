@@ -20,7 +20,7 @@ constexpr int kShipped = g256::kOptRound1;
 // tools/gemm_lab.py): 4096^3 98.9 -> 94.5 us (hipBLASLt 93.6), 8192^3
 // 739 -> 705 us (hipBLASLt 671).  Before: kSpacedMem (M G M M r M groups,
 // profiles/r3_gemm_lab_spaced.log).
-constexpr int kShippedW4 = g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore;
+constexpr long long kShippedW4 = g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore;
 constexpr int kW4MinK = 256;
 
 bool gemm256_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16) {

@@ -6,12 +6,12 @@
 
 namespace bk {
 
-constexpr int kShippedW4x = g4::kAsmMfma | g4::kInterleave;
+constexpr long long kShippedW4x = g4::kAsmMfma | g4::kInterleave;
 // the edge kernel runs the aligned kernel's two-barrier schedule and
 // non-temporal stores (gemm_bf16_256.hip kShippedW4; tools/gemm_lab.py
 // w4_asm_twobar_ntstore_edge).  (The [K][N] kernel keeps its schedule: with
 // kNtStore its f32-output instance spills 4 VGPRs.)
-constexpr int kShippedW4Edge = kShippedW4x | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore;
+constexpr long long kShippedW4Edge = kShippedW4x | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore;
 
 // the 4-wave 256x256 kernel on any M x N (K a multiple of 64): ragged
 // borders read zeros and store under a mask (g4::kEdge)

@@ -23,7 +23,7 @@ void run(const void* A, const void* B, void* C, int M, int N, int K, int lda, in
 }  // namespace
 
 // 4-wave 128x128-per-wave kernel options, lab ids 6..
-constexpr int kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave, g4::kNoCarry, g4::kDirectStore,
+constexpr long long kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave, g4::kNoCarry, g4::kDirectStore,
                            g4::kAsmMfma | g4::kInterleave, g4::kAsmMfma | g4::kNoCarry,
                            g4::kAsmMfma | g4::kInterleave | g4::kEarlyGlds,
                            g4::kAsmMfma | g4::kInterleave | g4::kReadsEarly,
@@ -70,7 +70,8 @@ constexpr int kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave, g4::kNoCarry, g4::
                                g4::kDiagNoVmWait | g4::kDiagNoBar2 | g4::kDiagNoBar1,
                            g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore | g4::kDiagNoReads0,
                            g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore | g4::kDiagNoGlds,
-                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kSwapAB};
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kSwapAB,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore | g4::kReads12};
 template <int I>
 void run_w4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool bf,
             hipStream_t s) {
@@ -142,6 +143,7 @@ BK_API int gemmlab_run(int variant, const void* A, const void* Bt, void* C, int 
     case 55: run_w4<49>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 56: run_w4<50>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 57: run_w4<51>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 58: run_w4<52>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     default: return kBadArgument;
   }
   return launch_status();
