@@ -18,7 +18,9 @@ to ordinary Python before the script is compiled:
   (a captured :class:`CommandResult`), ``$[cmd]`` (run, output not
   captured, ``None``) and ``![cmd]`` (run uncaptured, a result object);
 * inside a command, ``@(expr)`` interpolates a Python value (lists become
-  several arguments) and ``@$(cmd)`` splices a command's output as words.
+  several arguments) and ``@$(cmd)`` splices a command's output as words;
+* literals: path strings ``p"dir/f"`` / ``pf"{d}/f"`` (``pathlib.Path``)
+  and glob literals ``g`*.csv``` (the sorted list of matching paths).
 
 Command lines run under ``bash -c`` with the script's environment, so pipes,
 redirections, globs, ``&&``/``||`` and ``$VAR`` expansion behave as a shell's
@@ -61,7 +63,7 @@ _SOFT = {"match", "case", "_", "type"}
 def maybe_shell(source: str) -> bool:
     """Cheap screen (~15 us for a 40-line payload on the build host): False
     means the payload certainly has no xonsh construct."""
-    if "$" in source or "!(" in source or "![" in source:
+    if "$" in source or "!(" in source or "![" in source or _XSH_LITERAL.search(source):
         return True
     for m in _LINE.finditer("\n" + source + "\n"):
         head = m.group(1)
@@ -72,7 +74,11 @@ def maybe_shell(source: str) -> bool:
 
 # ---------------------------------------------------------------- scanning
 
-_STR_PREFIX = re.compile(r"(?i)(?:rb|br|fr|rf|r|b|f|u)?(?:'''|\"\"\"|'|\")")
+# string prefixes, xonsh's path strings (p, pr, rp, pf, fp) included
+_STR_PREFIX = re.compile(r"(?i)(?:rb|br|fr|rf|pr|rp|pf|fp|r|b|f|u|p)?(?:'''|\"\"\"|'|\")")
+# a path string (p"..."), or a glob literal (g`...`): not Python, so only a
+# payload with one of them (or another xonsh construct) is ever lowered
+_XSH_LITERAL = re.compile(r"(?<![\w.'\"])(?:[pP][rRfF]?|[rRfF][pP])['\"]|(?<![\w.])g`")
 _OPENERS = {"(": ")", "[": "]", "{": "}"}
 
 
@@ -81,7 +87,7 @@ def _skip_string(src: str, i: int) -> int:
     the end of the line for an unterminated one-quote string)."""
     m = _STR_PREFIX.match(src, i)
     assert m is not None
-    q = m.group(0).lstrip("rRbBfFuU")
+    q = m.group(0).lstrip("rRbBfFuUpP")
     j = m.end()
     n = len(src)
     while j < n:
@@ -185,9 +191,23 @@ def _lower_ops(text: str) -> str:
             continue
         if _string_start(text, i):
             j = _skip_string(text, i)
-            out.append(text[i:j])
+            lit = text[i:j]
+            prefix = _STR_PREFIX.match(text, i).group(0).rstrip("'\"")
+            if "p" in prefix.lower():
+                # xonsh path string: p"~/x" is pathlib.Path("~/x") (an f-string
+                # path formats first: pf"{d}/x")
+                rest = prefix.replace("p", "").replace("P", "") + lit[len(prefix):]
+                lit = f'__import__("pathlib").Path({rest})'
+            out.append(lit)
             i = j
             continue
+        if text.startswith("g`", i) and (i == 0 or not (text[i - 1].isalnum() or text[i - 1] in "_.")):
+            j = text.find("`", i + 2)
+            if j > 0 and "\n" not in text[i + 2:j]:
+                # xonsh glob literal: g`*.py` is the sorted list of matching paths
+                out.append(f"sorted(__import__('glob').glob({text[i + 2:j]!r}, recursive=True))")
+                i = j + 1
+                continue
         two = text[i:i + 2]
         if two in ("$(", "$[", "!(", "![", "${"):
             j = _match_close(text, i + 1)

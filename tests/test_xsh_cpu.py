@@ -233,3 +233,24 @@ def test_docstring_heavy_python_is_screened_by_one_parse():
     assert xsh.lower_payload(src) is None
     assert xsh._valid_python_needs_lowering("x = 1\nls -la\n")  # unbound bare name: a command
     assert xsh._valid_python_needs_lowering("echo $HOME\n")  # not Python at all
+
+
+def test_path_strings_and_glob_literals(tmp_path):
+    """xonsh's path strings (p"...", pf"..." formatting first) are
+    pathlib.Path objects and g`...` glob literals the sorted matches; valid
+    Python that merely contains such text in a string is untouched."""
+    (tmp_path / "a.txt").write_text("x")
+    (tmp_path / "b.txt").write_text("y")
+    r = run_script("""
+        d = p"data/sub"
+        print(type(d).__name__, d.parts)
+        name = "b"
+        f = pf"{name}.txt"
+        print(f.read_text())
+        print(g`*.txt`)
+        ls @(str(f))
+    """, tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.splitlines() == ["PosixPath ('data', 'sub')", "y", "['a.txt', 'b.txt']", "b.txt"], r.stdout
+    assert lower('s = "p\\"x\\" and g`y`"\nprint(s)\n') is None
+    assert lower("def f(p):\n    return p\nprint(f('q'))\n") is None
