@@ -47,8 +47,12 @@ constexpr int kRedMaxBlocks = 32768;
 // the old 8192-block grid: 175-178 us)
 constexpr int kRedBlocks = 512;
 constexpr int kRedUnroll = 16;
-// the fused RNG->reduce kernels are compute-bound: 4 blocks per CU
-constexpr int kRandRedMaxBlocks = 1024;
+// the fused RNG->reduce kernels are VALU-bound (80% of SIMD cycles issue
+// VALU, profiles/r4_payload_kernels_pmc.csv): 8 blocks per CU (8 waves per
+// SIMD) hide more of each Philox chain's latency -- 1e8 f64 square-sum
+// 91.3-91.5 us at 1024 blocks, 89.3-89.5 at 2048, 89.9-90.8 at 3072,
+// 90.5-91.2 at 4096, 101.9 at 8192 (profiles/r4_rand_reduce_sweep.jsonl)
+constexpr int kRandRedMaxBlocks = 2048;
 
 // lab overrides of grid targets (positive integers; anything else = default)
 inline int64_t env_int(const char* name, int64_t dflt) {
