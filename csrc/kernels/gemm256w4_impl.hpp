@@ -32,10 +32,12 @@
 // (>= 1024 cycles) to land, and every K-tile load has one whole iteration.
 // The only vmcnt(0) in the loop waits for loads issued an iteration earlier.
 //
-// Shipped options (gemm_bf16_256.hip): kAsmMfma | kInterleave = the same
-// loop with inline-asm MFMAs and an explicit issue order (ktile_asm below);
-// with builtin MFMAs the allocator moved accumulators through v_accvgpr_mov
-// in the loop and the kernel lost to the 8-wave one.
+// Shipped options (gemm_bf16_256.hip): kAsmMfma | kInterleave with the
+// two-barrier K-loop (kTwoBar | kTwoBarG10, ktile_asm2 below: the wait for
+// the next K-tile sits in the second k-half, not at the k-half boundary
+// sketched above) and non-temporal C stores (kNtStore).  Inline-asm MFMAs:
+// with builtin MFMAs the allocator moved accumulators through
+// v_accvgpr_mov in the loop and the kernel lost to the 8-wave one.
 #pragma once
 #include "bk_common.hpp"
 
