@@ -185,11 +185,11 @@ def cpu_usage_s():
     return (sum(v) - v[3] - v[4]) / os.sysconf("SC_CLK_TCK"), "procstat"
 
 
-def cpu_throttle() -> dict:
+def cpu_throttle(paths=(("/sys/fs/cgroup/cpu.stat", 1.0), ("/sys/fs/cgroup/cpu/cpu.stat", 1e-3))) -> dict:
     """The container's CFS bandwidth counters (cgroup v2 cpu.stat or v1
     cpu/cpu.stat): enforcement periods, periods in which the quota ran out,
     and the time processes sat throttled -- {} without a quota."""
-    for path, scale in (("/sys/fs/cgroup/cpu.stat", 1.0), ("/sys/fs/cgroup/cpu/cpu.stat", 1e-3)):
+    for path, scale in paths:
         try:
             with open(path) as f:
                 kv = dict(line.split() for line in f if len(line.split()) == 2)

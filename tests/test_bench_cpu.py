@@ -145,3 +145,23 @@ def test_gang_check_is_bounded_and_stops_at_the_first_failure(monkeypatch):
     monkeypatch.setenv("BEE_BENCH_GANG_BUDGET_S", "10")
     out = bench.gang_allreduce_check("127.0.0.1:1", 8, repeats=2, hport=None)
     assert calls == [] and "budget" in out.get("skipped", ""), out
+
+
+def test_cpu_throttle_reads_both_cgroup_versions(tmp_path):
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod2", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    v2 = tmp_path / "v2.stat"
+    v2.write_text("usage_usec 10\nnr_periods 40\nnr_throttled 3\nthrottled_usec 25000\n")
+    v1 = tmp_path / "v1.stat"
+    v1.write_text("nr_periods 7\nnr_throttled 1\nthrottled_time 2000000\n")
+    a = bench.cpu_throttle(((str(tmp_path / "missing"), 1.0), (str(v2), 1.0)))
+    assert a == {"periods": 40, "throttled": 3, "throttled_ms": 25.0}
+    b = bench.cpu_throttle(((str(v1), 1e-3),))
+    assert b == {"periods": 7, "throttled": 1, "throttled_ms": 2.0}
+    assert bench.cpu_throttle(((str(tmp_path / "missing"), 1.0),)) == {}
+    d = bench.throttle_delta(a, {"periods": 50, "throttled": 5, "throttled_ms": 40.0})
+    assert d == {"periods": 10, "throttled_periods": 2, "throttled_ms": 15.0}
+    assert bench.throttle_delta({}, a) is None
