@@ -3,7 +3,7 @@
   1. hello_world on a CPU-only executor                  (--cpu-only)
   2. benchmark-fib on 1 GPU-pinned executor
   3. benchmark-numpy via HIP kernels on 1 GPU (headline)  + the unmodified
-     numpy payload on CPU in the same pod, for comparison
+     numpy payload on CPU in the same pod, and under the numpy offload
   4./5. (8 GPUs: 64 concurrent Executes, gang all-reduce) are the driver's
      N=8 bench.py run; on the 1-GPU box they are skipped.
 
@@ -24,6 +24,8 @@ RUNS = [
     ("fib_gpu_pod", ["--workload", "fib", "--steps", "4", "--concurrency", "16"]),
     ("numpy_gpu", ["--workload", "numpy_gpu", "--steps", "30"]),
     ("numpy_cpu", ["--workload", "numpy_cpu", "--steps", "3", "--concurrency", "4"]),
+    # the same unmodified payload with the opt-in numpy offload (ops/numpy_offload.py)
+    ("numpy_cpu_offload", ["--workload", "numpy_cpu", "--numpy-offload", "--steps", "30"]),
     ("scientific_gpu_pod", ["--workload", "scientific", "--steps", "30"]),
 ]
 
