@@ -199,8 +199,9 @@ bool SandboxPool::start(std::string* err) {
   // initialises HIP itself, on its pinned device
   const bool cpu_light = !want_broker && !cfg_.pod_mode && cfg_.light_target > 0 && cfg_.light_zygotes > 0;
   const int nl = want_broker || cpu_light ? std::max(1, cfg_.light_zygotes) : 0;
-  const int nm = nl > 0 && cfg_.min_target > 0 ? cfg_.min_zygotes : 0;
-  const int nn = nl > 0 && cfg_.nano_target > 0 ? cfg_.nano_zygotes : 0;
+  // (no broker: the *_cpu kinds are served by the base kinds' zygotes, target_of)
+  const int nm = nl > 0 && (cfg_.min_target > 0 || (!want_broker && cfg_.min_cpu_target > 0)) ? cfg_.min_zygotes : 0;
+  const int nn = nl > 0 && (cfg_.nano_target > 0 || (!want_broker && cfg_.nano_cpu_target > 0)) ? cfg_.nano_zygotes : 0;
   for (int i = 0; i < 1 + nl + nm + nn; ++i) {
     auto z = std::make_unique<Zygote>();
     z->index = i;
@@ -936,10 +937,17 @@ std::vector<std::shared_ptr<Worker>> SandboxPool::take_gang_locked(const std::st
 }
 
 int SandboxPool::target_of(int kind) const {
+  // without a broker (CPU-only pools) the *_cpu kinds fold into their base
+  // kind (handle(): mode "nano_cpu" -> kNano), so the base pool is sized for
+  // both: a CPU-only node's stdlib scripts otherwise queue on the few warm
+  // sandboxes of the GPU-script pool (hello on a CPU-only executor: p50
+  // acquire 1.2 ms, 2755 vs 4531 RPS GPU-pinned, profiles/r4_bench_suite.jsonl)
   if (kind == kLight) return light_ok_ ? cfg_.light_target : 0;
-  if (kind == kMin) return light_ok_ && min_ok_ ? cfg_.min_target : 0;
+  if (kind == kMin)
+    return light_ok_ && min_ok_ ? (!broker_ ? std::max(cfg_.min_target, cfg_.min_cpu_target) : cfg_.min_target) : 0;
   if (kind == kMinCpu) return broker_ && min_ok_ ? (cfg_.min_cpu_target >= 0 ? cfg_.min_cpu_target : cfg_.min_target) : 0;
-  if (kind == kNano) return light_ok_ && nano_ok_ ? cfg_.nano_target : 0;
+  if (kind == kNano)
+    return light_ok_ && nano_ok_ ? (!broker_ ? std::max(cfg_.nano_target, cfg_.nano_cpu_target) : cfg_.nano_target) : 0;
   if (kind == kNanoCpu)
     return broker_ && nano_ok_ ? (cfg_.nano_cpu_target >= 0 ? cfg_.nano_cpu_target : cfg_.nano_target) : 0;
   return cfg_.target;

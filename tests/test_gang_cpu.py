@@ -133,3 +133,38 @@ def test_gang_ranks_get_the_operator_rccl_env(tmp_path):
     assert gang["exit_code"] == 0, gang["stderr"]
     assert sorted(gang["stdout"].splitlines()) == ["0 1 LL128", "1 1 LL128"], gang["stdout"]
     assert one["stdout"] == "None None None\n", one
+
+
+def test_cpu_only_pools_take_the_cpu_targets(tmp_path):
+    """Without a broker the nano_cpu / min_cpu kinds fold into nano / min
+    (stdlib scripts run in the nano pool), so those pools are sized for the
+    CPU-only targets too rather than for the GPU-script ones -- and a zygote
+    of the kind starts even when only the *_cpu target is set."""
+    ensure_native_executor()
+
+    async def go(extra):
+        ex = ExecutorProcess("cpuonly", str(tmp_path / f"sb{len(extra)}"), gpus="", target=1,
+                             light_target=1, light_zygotes=1,
+                             extra_args=["--min-zygotes", "1", "--nano-zygotes", "1", *extra])
+        await ex.start()
+        try:
+            await ex.wait_ready(1, 120)
+            for _ in range(600):
+                st = await ex.get_json("/v1/status")
+                if st["ready_nano"] >= st["nano_target"] and st["ready_min"] >= st["min_target"]:
+                    break
+                await asyncio.sleep(0.1)
+            r = await ex.post("/v1/execute", {"source_code": "print(6)", "mode": "nano_cpu"}, timeout=60)
+            return st, r.json()
+        finally:
+            await ex.close()
+
+    st, body = asyncio.run(go(["--nano-target", "1", "--nano-cpu-target", "3", "--min-target", "1",
+                               "--min-cpu-target", "2"]))
+    assert st["nano_cpu_target"] == 0 and st["min_cpu_target"] == 0, st  # no broker: no *_cpu pools
+    assert st["nano_target"] == 3 and st["min_target"] == 2, st
+    assert st["ready_nano"] == 3 and st["ready_min"] == 2, st
+    assert body["stdout"] == "6\n"
+    st, body = asyncio.run(go(["--nano-target", "0", "--nano-cpu-target", "2", "--min-target", "0"]))
+    assert st["nano_target"] == 2 and st["ready_nano"] == 2 and st["min_target"] == 0, st
+    assert body["stdout"] == "6\n"
