@@ -132,6 +132,7 @@ class GrpcServer:
         )
         self.server_credentials = server_credentials
         self.bound_port: Optional[int] = None
+        self.peer_guard = getattr(servicer, "peer_guard", None)  # learns the ports bound below
         services = [pb.CI_SERVICE, pb.HEALTH_SERVICE] + [f"{p}.ServerReflection" for p in pb.REFLECTION_FILES]
         ci = {
             "Execute": _unary(servicer.Execute, pb.ExecuteRequest, pb.ExecuteResponse),
@@ -179,6 +180,8 @@ class GrpcServer:
         else:
             logger.info("Starting server on secure port %s", listen_addr)
             self.bound_port = self.server.add_secure_port(listen_addr, self.server_credentials)
+        if self.peer_guard is not None and self.bound_port:
+            self.peer_guard.ports.add(self.bound_port)
         return self.bound_port
 
     async def start(self, listen_addr: Optional[str] = None) -> None:

@@ -1,0 +1,213 @@
+"""Refuse API calls that come from this node's own sandboxes.
+
+The reference gives every execution its own pod, so user code reaches the
+service only the way any other cluster client would
+(`/root/reference/src/code_interpreter/services/kubernetes_code_executor.py:220-253`).
+Here sandboxes share the node's loopback: with the default network policy
+("open", config.sandbox_network) a sandbox could connect to the service's
+own gRPC / HTTP listeners and start executions, upload or delete objects.
+The Landlock TCP layer that denies those ports costs ~13 ms of CPU per
+sandbox (config.sandbox_net_layer), so it is opt-in.
+
+This guard costs nothing per sandbox: in UID mode every sandbox process
+runs under a UID of the service's sandbox range, and the kernel knows the
+owner of every local TCP socket.  For each call whose peer is a socket on
+this host, one NETLINK_SOCK_DIAG exact lookup (~5-15 us) returns the peer
+socket's UID; a UID in the sandbox range gets PERMISSION_DENIED / 403.
+Peers that are not local sockets (other hosts) are not looked up further.
+A peer that claims a local address but whose socket cannot be found is
+refused (fail closed).
+"""
+
+from __future__ import annotations
+
+import ipaddress
+import logging
+import os
+import socket
+import struct
+import threading
+import time
+from typing import Iterable, List, Optional, Set, Tuple
+
+logger = logging.getLogger("peer_guard")
+
+NETLINK_SOCK_DIAG = 4
+SOCK_DIAG_BY_FAMILY = 20
+NLMSG_ERROR = 2
+NLM_F_REQUEST = 1
+_NOCOOKIE = 0xFFFFFFFF
+_ALL_STATES = 0xFFFFFFFF
+# struct inet_diag_msg: family, state, timer, retrans (4 x u8), inet_diag_sockid
+# (48 bytes), expires, rqueue, wqueue, uid, inode (5 x u32): uid at 64
+_UID_OFF = 4 + 48 + 12
+
+
+def _addr16(family: int, ip: str) -> bytes:
+    return socket.inet_pton(family, ip).ljust(16, b"\0")
+
+
+class SockDiag:
+    """Exact lookups of one local TCP socket by its 4-tuple (one netlink
+    socket per thread; the front-end calls from its event loop thread)."""
+
+    def __init__(self) -> None:
+        self._tls = threading.local()
+        self._seq = 0
+
+    def _sock(self) -> socket.socket:
+        s = getattr(self._tls, "s", None)
+        if s is None:
+            s = socket.socket(socket.AF_NETLINK, socket.SOCK_DGRAM, NETLINK_SOCK_DIAG)
+            s.settimeout(1.0)
+            self._tls.s = s
+        return s
+
+    def uid(self, family: int, src: str, sport: int, dst: str, dport: int) -> Optional[int]:
+        """UID of the TCP socket whose local end is (src, sport) and remote
+        end (dst, dport); None when there is no such socket on this host."""
+        sockid = struct.pack("!HH", sport, dport) + _addr16(family, src) + _addr16(family, dst)
+        sockid += struct.pack("=III", 0, _NOCOOKIE, _NOCOOKIE)  # any interface, no cookie
+        req = struct.pack("=BBBBI", family, socket.IPPROTO_TCP, 0, 0, _ALL_STATES) + sockid
+        self._seq = (self._seq + 1) & 0x7FFFFFFF
+        msg = struct.pack("=IHHII", 16 + len(req), SOCK_DIAG_BY_FAMILY, NLM_F_REQUEST, self._seq, 0) + req
+        s = self._sock()
+        s.sendto(msg, (0, 0))
+        data = s.recv(8192)
+        _, typ = struct.unpack_from("=IH", data)
+        if typ != SOCK_DIAG_BY_FAMILY or len(data) < 16 + _UID_OFF + 4:
+            return None  # NLMSG_ERROR: ENOENT (no such socket here)
+        return struct.unpack_from("=I", data, 16 + _UID_OFF)[0]
+
+
+def local_addresses() -> Set[str]:
+    """This host's own IPv4 / IPv6 addresses (network namespace), from
+    procfs: the fib's LOCAL host routes and if_inet6."""
+    out: Set[str] = {"127.0.0.1", "::1"}
+    try:
+        with open("/proc/net/fib_trie") as fh:
+            prev = None
+            for line in fh:
+                parts = line.split()
+                if "/32 host LOCAL" in line and prev:
+                    out.add(prev)
+                if len(parts) == 2 and parts[0] in ("|--", "+--"):
+                    prev = parts[1]
+    except OSError:
+        pass
+    try:
+        with open("/proc/net/if_inet6") as fh:
+            for line in fh:
+                h = line.split()[0]
+                out.add(str(ipaddress.IPv6Address(bytes.fromhex(h))))
+    except (OSError, ValueError, IndexError):
+        pass
+    return out
+
+
+def parse_peer(peer: str) -> Optional[Tuple[int, str, int]]:
+    """gRPC's ``context.peer()`` ("ipv4:1.2.3.4:5", "ipv6:[::1]:5",
+    "ipv6:[::ffff:127.0.0.1]:5") -> (family, ip, port); None for others
+    (unix sockets)."""
+    try:
+        kind, _, rest = peer.partition(":")
+        if kind == "ipv4":
+            ip, _, port = rest.rpartition(":")
+            return socket.AF_INET, ip, int(port)
+        if kind == "ipv6":
+            ip, _, port = rest.rpartition(":")
+            ip = ip.strip("[]").split("%", 1)[0]
+            return normalise(socket.AF_INET6, ip, int(port))
+    except ValueError:
+        return None
+    return None
+
+
+def normalise(family: int, ip: str, port: int) -> Tuple[int, str, int]:
+    """IPv4-mapped IPv6 peers are AF_INET sockets on their side."""
+    if family == socket.AF_INET6:
+        a = ipaddress.IPv6Address(ip)
+        if a.ipv4_mapped is not None:
+            return socket.AF_INET, str(a.ipv4_mapped), port
+        return socket.AF_INET6, str(a), port
+    return family, ip, port
+
+
+class PeerGuard:
+    """``refuse(family, ip, port, server=None)`` -> a reason string when the
+    caller is a sandbox of this node, else None."""
+
+    def __init__(self, uid_ranges: Iterable[Tuple[int, int]], ports: Iterable[int] = ()) -> None:
+        self.uid_ranges: List[Tuple[int, int]] = list(uid_ranges)
+        self.ports: Set[int] = set(ports)  # the service's listening ports (gRPC peers carry no local end)
+        self.diag = SockDiag()
+        self.local = local_addresses()
+        self._local_at = time.monotonic()
+        self.refused_total = 0
+
+    def is_sandbox_uid(self, uid: int) -> bool:
+        return any(lo <= uid < hi for lo, hi in self.uid_ranges)
+
+    def _peer_uid(self, family: int, ip: str, port: int, server: Optional[Tuple[str, int]]) -> Tuple[bool, Optional[int]]:
+        """(local, uid): whether (ip, port) is a socket address of this host
+        and, if its socket was found, its owner."""
+        loop = ipaddress.ip_address(ip).is_loopback
+        if not loop and ip not in self.local and time.monotonic() - self._local_at > 10.0:
+            # an address the node gained since the last read (pod IP change)
+            self.local, self._local_at = local_addresses(), time.monotonic()
+        if not loop and ip not in self.local:
+            return False, None
+        cands: List[Tuple[str, int]] = []
+        if server is not None:
+            sf, sip, sport = normalise(socket.AF_INET6 if ":" in server[0] else socket.AF_INET, server[0], server[1])
+            if sf == family:
+                cands.append((sip, sport))
+        if not cands:
+            # gRPC: the connection's local end is not exposed; a local client
+            # reaches a listener through the address it connects from
+            # (loopback to itself, the node's address to itself), else any
+            # of the node's addresses
+            same = [a for a in self.local if (":" in a) == (family == socket.AF_INET6)]
+            order = [ip] + sorted(a for a in same if a != ip)
+            cands = [(a, p) for a in order for p in sorted(self.ports)]
+        for dst, dport in cands:
+            uid = self.diag.uid(family, ip, port, dst, dport)
+            if uid is not None:
+                return True, uid
+        return True, None
+
+    def refuse(self, family: int, ip: str, port: int, server: Optional[Tuple[str, int]] = None) -> Optional[str]:
+        if not self.uid_ranges:
+            return None
+        try:
+            family, ip, port = normalise(family, ip, port)
+            local, uid = self._peer_uid(family, ip, port, server)
+        except (OSError, ValueError) as e:  # netlink unavailable: the Landlock layer is the control
+            logger.warning("peer guard: lookup failed (%s); allowing %s:%d", e, ip, port)
+            return None
+        if not local:
+            return None
+        if uid is None:
+            self.refused_total += 1
+            return f"local peer {ip}:{port} without a findable socket"
+        if self.is_sandbox_uid(uid):
+            self.refused_total += 1
+            return f"calls from sandboxes of this node are refused (peer uid {uid})"
+        return None
+
+    def refuse_grpc_peer(self, peer: str) -> Optional[str]:
+        p = parse_peer(peer)
+        return self.refuse(*p) if p is not None else None
+
+
+def sandbox_uid_ranges(config) -> List[Tuple[int, int]]:
+    """The UIDs sandboxes of this node run under (UID mode: a root service
+    with sandbox_uid_base set), one block of sandbox_uid_count per slot; []
+    when sandboxes share the service's UID (then the guard cannot tell them
+    apart and the Landlock options are the control)."""
+    if (config.executor_backend or "").lower() != "local" or (config.sandbox_isolation or "auto").lower() == "off":
+        return []
+    if config.sandbox_uid_base <= 0 or os.geteuid() != 0:
+        return []
+    slots = max(len(config.gpu_ids or []), 64)  # slot i: base + i * count (local_gpu_pool.isolation_args)
+    return [(config.sandbox_uid_base, config.sandbox_uid_base + config.sandbox_uid_count * slots)]
