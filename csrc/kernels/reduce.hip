@@ -44,7 +44,12 @@ constexpr int kRedMaxBlocks = 32768;
 // grid-stride layout 167 / 135 / 141 / 154 / 164 / 178 us at 256 / 512 / 768 /
 // 1024 / 2048 / 4096 blocks, block-contiguous 168 / 142 / 145 / 145 / 157 /
 // 158; torch.sum over the same 800 MB 139 us (profiles/r4_reduce_sweep*.jsonl;
-// the old 8192-block grid: 175-178 us)
+// the old 8192-block grid: 175-178 us).  Round 4 (profiles/r4_reduce_layout_sweep.jsonl,
+// interleaved): the LDS-DMA stream below 140-145 us at its best grid (256
+// blocks), the same as this kernel at 512; 4 or 8 loads in flight per lane
+// instead of 16 at 512 / 1024 / 2048 blocks: 137.7 / 164-167 / 166-172 us --
+// the grid (8 waves per CU), not the bytes in flight, sets the rate, and
+// ~5.8 TB/s (torch.sum's too) is this read stream's ceiling on these boxes
 constexpr int kRedBlocks = 512;
 constexpr int kRedUnroll = 16;
 // the fused RNG->reduce kernels are VALU-bound (80% of SIMD cycles issue
@@ -169,13 +174,12 @@ __device__ __forceinline__ void finish(double v, double* partials, unsigned* tic
   }
 }
 
-template <typename T, int OP, bool NT>
+template <typename T, int OP, bool NT, int U = kRedUnroll>  // U: 16-B loads in flight per lane
 __global__ __launch_bounds__(kRedBlock) void reduce_1pass(const T* __restrict__ a, const T* __restrict__ b, int64_t n,
                                                          double* __restrict__ partials, unsigned* __restrict__ ticket,
                                                          double* __restrict__ out) {
   using V = V16<T>;
   constexpr int N = 16 / sizeof(T);
-  constexpr int U = kRedUnroll;  // 16-B loads in flight per lane
   const int64_t nvec = n / N;
   const int64_t stride = (int64_t)gridDim.x * kRedBlock;
   const int64_t tid = (int64_t)blockIdx.x * kRedBlock + threadIdx.x;
@@ -301,6 +305,101 @@ __global__ __launch_bounds__(kRedBlock) void reduce_chunked(const T* __restrict_
   finish<OP>(block_reduce<OP>(v), partials, ticket, out);
 }
 
+// LDS-DMA stream: each wave walks one contiguous run of 1-KiB pieces (a
+// wave's 64 lanes x 16 B) through a private ring of kDmaSlots pieces in LDS,
+// filled by `global_load_lds_dwordx4` (non-temporal for arrays past the
+// Infinity Cache), kDmaSlots pieces in flight; it reads its own lanes' 16 B
+// back with ds_read_b128 once the covering `s_waitcnt vmcnt` says they
+// landed.  MI355X_MICROARCH.md measures an LDS-DMA stream at 6.4 TB/s
+// (6.5-6.8 nt) against ~6.3 for register-staged copies; the register-load
+// kernels above reach 5.7 TB/s on this reduction (torch.sum 5.8,
+// profiles/r4_reduce_sweep3.jsonl).  Measured, it does not beat them: 144-145
+// us per-wave contiguous, 139-141 us with grid-strided pieces (STRIDED), both
+// at 256 blocks; slower at 512+ (profiles/r4_reduce_layout_sweep.jsonl).  A lab
+// layout (BK_REDUCE_LAYOUT=ldsdma / ldsdma_stride), exact against fp64 numpy
+// (tools/probe/reduce_layout_check.py).  Only the issuing wave reads a slot, so
+// no barrier orders the ring: vmcnt before the read, lgkmcnt(0) before the
+// slot's next fill.  The DMA is inline asm so the compiler neither tracks it
+// nor inserts its own vmcnt(0) ahead of every LDS read (the GEMM's reason,
+// gemm256w4_impl.hpp glds_raw).  Single-operand ops (the payload's
+// square-sum); the loads use 64-bit addresses (no 4 GiB buffer limit).
+constexpr int kDmaSlots = 16;  // pieces in flight per wave (16 KiB of LDS per wave, 64 KiB per block)
+constexpr int kDmaGroup = 4;   // pieces retired per wait
+typedef __attribute__((address_space(3))) void* red_lds_ptr;
+
+template <bool NT>
+__device__ __forceinline__ void dma_piece(const void* src, unsigned lds_addr) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(lds_addr);
+  // s_nop 0: one wait state between the M0 write and the LDS-DMA load
+  if constexpr (NT)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt" ::"s"(m0), "v"(src) : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(src) : "memory", "m0");
+}
+
+template <typename T, int OP, bool NT, bool STRIDED>
+__global__ __launch_bounds__(kRedBlock) void reduce_ldsdma(const T* __restrict__ a, int64_t n,
+                                                          double* __restrict__ partials, unsigned* __restrict__ ticket,
+                                                          double* __restrict__ out) {
+  static_assert(!kTwoOperands<OP>, "single-operand reductions");
+  constexpr int N = 16 / sizeof(T);
+  constexpr int S = kDmaSlots, G = kDmaGroup;
+  __shared__ __attribute__((aligned(1024))) char ring[kRedBlock / kWave][S * 1024];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t pieces = n / (N * kWave);  // whole 1-KiB pieces
+  const int64_t waves = (int64_t)gridDim.x * (kRedBlock / kWave);
+  const int64_t per = (pieces + waves - 1) / waves;
+  const int64_t w = (int64_t)blockIdx.x * (kRedBlock / kWave) + wid;
+  // STRIDED: wave w takes pieces w, w + waves, ... (the whole chip sweeps one
+  // contiguous front, as the grid-stride kernel does); else one contiguous run
+  const int64_t p0 = STRIDED ? w : (w * per < pieces ? w * per : pieces);
+  const int64_t np = STRIDED ? (w < pieces ? (pieces - w + waves - 1) / waves : 0)
+                             : (p0 + per < pieces ? p0 + per : pieces) - p0;
+  const int64_t step = STRIDED ? waves * 1024 : 1024;  // bytes from one of this wave's pieces to the next
+  const char* src = reinterpret_cast<const char*>(a) + p0 * 1024 + lane * 16;
+  const unsigned base = (unsigned)(unsigned long long)(red_lds_ptr)(&ring[wid][0]);
+  const char* mine = &ring[wid][lane * 16];
+  double acc[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) acc[g] = red_init<OP>();
+  auto take = [&](double& r, int slot) {
+    const V16<T> v = *reinterpret_cast<const V16<T>*>(mine + slot * 1024);
+#pragma unroll
+    for (int q = 0; q < N; ++q) r = red_combine<OP>(r, red_map<OP>(to_f64<T>(v.v[q]), 0.0));
+  };
+  const int64_t first = np < S ? np : S;
+  for (int64_t j = 0; j < first; ++j) dma_piece<NT>(src + j * step, base + (unsigned)j * 1024);
+  int64_t j = 0;
+  // steady state: exactly S pieces in flight before each wait
+  for (; j + S + G <= np; j += G) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S - G) : "memory");
+#pragma unroll
+    for (int g = 0; g < G; ++g) take(acc[g], (int)((j + g) % S));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slots' reads are done before their refill
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      dma_piece<NT>(src + (j + S + g) * step, base + (unsigned)((j + g) % S) * 1024);
+  }
+  // the rest: everything issued so far lands, then the pieces never issued
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int64_t issued = j + S < np ? j + S : np;
+  for (int64_t k = j; k < issued; ++k) take(acc[0], (int)(k % S));
+  for (int64_t k = issued; k < np; ++k) {
+    const V16<T> v = ld16<NT>(reinterpret_cast<const V16<T>*>(src + k * step));
+#pragma unroll
+    for (int q = 0; q < N; ++q) acc[0] = red_combine<OP>(acc[0], red_map<OP>(to_f64<T>(v.v[q]), 0.0));
+  }
+  // elements past the last whole piece: the grid's last block
+  if (blockIdx.x == gridDim.x - 1)
+    for (int64_t k = pieces * N * kWave + threadIdx.x; k < n; k += kRedBlock)
+      acc[0] = red_combine<OP>(acc[0], red_map<OP>(to_f64<T>(a[k]), 0.0));
+  double v = acc[0];
+#pragma unroll
+  for (int g = 1; g < G; ++g) v = red_combine<OP>(v, acc[g]);
+  finish<OP>(block_reduce<OP>(v), partials, ticket, out);
+}
+
 // ---- fused RNG -> reduce -------------------------------------------------------
 // sum / square-sum over a uniform Philox stream WITHOUT materialising it:
 // element i takes exactly the value philox_uniform_{f64,f32} would store
@@ -374,12 +473,34 @@ int launch_reduce(const void* a, const void* b, int64_t n, double* workspace, do
   if (g > (unsigned)red_blocks) g = (unsigned)red_blocks;  // the workspace holds kRedMaxBlocks partials
   unsigned* ticket = reinterpret_cast<unsigned*>(workspace + kRedMaxBlocks);
   static const bool chunked = getenv("BK_REDUCE_LAYOUT") && !strcmp(getenv("BK_REDUCE_LAYOUT"), "chunk");
+  static const bool ldsdma = getenv("BK_REDUCE_LAYOUT") && !strcmp(getenv("BK_REDUCE_LAYOUT"), "ldsdma");
+  static const bool ldsdma_s = getenv("BK_REDUCE_LAYOUT") && !strcmp(getenv("BK_REDUCE_LAYOUT"), "ldsdma_stride");
   const bool nt = stream_nt(n * (int64_t)sizeof(T) * (kTwoOperands<OP> ? 2 : 1));
+  if constexpr (!kTwoOperands<OP>) {
+    if (ldsdma || ldsdma_s) {
+      if (ldsdma_s) {
+        if (nt) reduce_ldsdma<T, OP, true, true><<<g, kRedBlock, 0, s>>>((const T*)a, n, workspace, ticket, out);
+        else reduce_ldsdma<T, OP, false, true><<<g, kRedBlock, 0, s>>>((const T*)a, n, workspace, ticket, out);
+      } else if (nt) {
+        reduce_ldsdma<T, OP, true, false><<<g, kRedBlock, 0, s>>>((const T*)a, n, workspace, ticket, out);
+      } else {
+        reduce_ldsdma<T, OP, false, false><<<g, kRedBlock, 0, s>>>((const T*)a, n, workspace, ticket, out);
+      }
+      return launch_status();
+    }
+  }
   if (chunked) {
     if (nt) reduce_chunked<T, OP, true><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
     else reduce_chunked<T, OP, false><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
   } else if (nt) {
-    reduce_1pass<T, OP, true><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
+    // lab: BK_REDUCE_UNROLL=4/8 -- fewer loads in flight per lane, for grids with more waves
+    static const int unroll = (int)env_int("BK_REDUCE_UNROLL", kRedUnroll);
+    if (unroll == 4)
+      reduce_1pass<T, OP, true, 4><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
+    else if (unroll == 8)
+      reduce_1pass<T, OP, true, 8><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
+    else
+      reduce_1pass<T, OP, true><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
   } else {
     reduce_1pass<T, OP, false><<<g, kRedBlock, 0, s>>>((const T*)a, (const T*)b, n, workspace, ticket, out);
   }

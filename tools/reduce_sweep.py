@@ -69,11 +69,23 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=10**8)
     ap.add_argument("--reps", type=int, default=30)
+    # reduce.hip reduce_1pass (stride) / reduce_chunked (chunk) / reduce_ldsdma (ldsdma)
+    ap.add_argument("--layouts", default="stride,chunk")
+    ap.add_argument("--blocks", default="384,512,640,768,1024")
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--unrolls", default="16", help="BK_REDUCE_UNROLL values (grid-stride layout: 4 / 8 / 16)")
+    ap.add_argument("--no-refs", action="store_true", help="skip the Philox store / torch / copy reference rows")
     a = ap.parse_args()
-    for _ in range(2):  # interleaved repeats: box-to-box and run-to-run noise is a few %
-        for layout in ("stride", "chunk"):  # reduce.hip reduce_1pass vs reduce_chunked
-            for blocks in (384, 512, 640, 768, 1024):
-                run("square_sum", {"BK_REDUCE_BLOCKS": str(blocks), "BK_REDUCE_LAYOUT": layout}, a.n, a.reps)
+    for _ in range(a.rounds):  # interleaved repeats: box-to-box and run-to-run noise is a few %
+        for layout in a.layouts.split(","):
+            for blocks in a.blocks.split(","):
+                for u in (a.unrolls.split(",") if layout == "stride" else ["16"]):
+                    env = {"BK_REDUCE_BLOCKS": blocks, "BK_REDUCE_LAYOUT": layout}
+                    if u != "16":
+                        env["BK_REDUCE_UNROLL"] = u
+                    run("square_sum", env, a.n, a.reps)
+    if a.no_refs:
+        return
     run("philox_store", {}, a.n, a.reps)
     run("torch_sum", {}, a.n, a.reps)   # torch's own reduction over the same 800 MB (read roofline reference)
     run("d2d_copy", {}, a.n, a.reps)    # hipMemcpy device-to-device: 800 MB read + 800 MB written  # (its grid is fixed: kDrawBlocksPerCU, profiles/archive/r3_philox_grid_sweep.log)
