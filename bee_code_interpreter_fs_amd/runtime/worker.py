@@ -294,16 +294,21 @@ def load_precompiled(blob: str, path: str):
     return rename(code), raw[len(magic): len(magic) + 1] == b"X"
 
 
-def _run_main(path: str, lowered: Optional[str] = None, code=None, shell: bool = False) -> None:
+def _run_main(path: str, lowered: Optional[str] = None, code=None, shell: bool = False,
+              raw: Optional[bytes] = None) -> None:
     """`python path` semantics (what runpy.run_path does for a plain file,
     minus its zip/directory probing): compile, bind a fresh ``__main__``
     module, execute.  ``lowered``: the payload with its xonsh shell lines
     lowered to Python (runtime/xsh.py), compiled under the same file name so
-    tracebacks point at the user's lines.  The module is left alive -- the
+    tracebacks point at the user's lines.  ``raw``: the file's bytes when the
+    caller already read them (compile() honours a coding cookie in bytes, as
+    for the file).  The module is left alive -- the
     process ends with os._exit, and the broker releases device memory on
     disconnect -- so no teardown work lands on the request path."""
     if code is None:
-        if lowered is None:
+        if lowered is None and raw is not None:
+            source = raw
+        elif lowered is None:
             with io.open_code(path) as fh:
                 source = fh.read()
         else:
@@ -362,19 +367,26 @@ def run_script(script: str, argv, workspace: str, runtime_packages: str, precomp
 
         numpy_offload.install()
     lowered = None
+    raw = None
     pre = load_precompiled(precompiled, script) if precompiled else None
+    # the dependency guesser needs the source only with a wheelhouse to install from
+    guess = bool(os.environ.get("BEE_WHEELHOUSE"))
     try:
-        with open(script, "rb") as fh:
-            source = fh.read().decode("utf-8", errors="replace")
-        from . import xsh
-        from .deps import install_missing
+        if pre is None or guess:
+            # read once: the lowering, the guesser and the compile share it
+            with io.open_code(script) as fh:
+                raw = fh.read()
+            source = raw.decode("utf-8", errors="replace")
+            from . import xsh
+            from .deps import install_missing
 
-        # xonsh-style shell lines (the reference ran every payload through
-        # xonsh): lowered to Python here, plain Python passes untouched --
-        # unless the front-end already compiled the payload (lowering included)
-        if pre is None:
-            lowered = xsh.lower_payload(source)
-        install_missing(lowered or source, runtime_packages)
+            # xonsh-style shell lines (the reference ran every payload through
+            # xonsh): lowered to Python here, plain Python passes untouched --
+            # unless the front-end already compiled the payload (lowering included)
+            if pre is None:
+                lowered = xsh.lower_payload(source)
+            if guess:
+                install_missing(lowered or source, runtime_packages)
     except OSError:
         pass
     code = 0
@@ -383,7 +395,7 @@ def run_script(script: str, argv, workspace: str, runtime_packages: str, precomp
         if pre is not None:
             _run_main(script, code=pre[0], shell=pre[1])
         else:
-            _run_main(script, lowered)
+            _run_main(script, lowered, raw=raw)
     except SystemExit as e:
         if e.code is None:
             code = 0

@@ -254,3 +254,19 @@ def test_path_strings_and_glob_literals(tmp_path):
     assert r.stdout.splitlines() == ["PosixPath ('data', 'sub')", "y", "['a.txt', 'b.txt']", "b.txt"], r.stdout
     assert lower('s = "p\\"x\\" and g`y`"\nprint(s)\n') is None
     assert lower("def f(p):\n    return p\nprint(f('q'))\n") is None
+
+
+def test_literal_screen_matches_its_regex():
+    """maybe_shell's quote-walking screen (_has_xsh_literal) is the
+    _XSH_LITERAL regex's search, without the per-position lookbehind."""
+    import random
+
+    from bee_code_interpreter_fs_amd.runtime import xsh
+
+    rnd = random.Random(7)
+    alpha = "pPrRfFgxy_.'\"` \n1é"
+    for _ in range(50000):
+        s = "".join(rnd.choice(alpha) for _ in range(rnd.randint(0, 9)))
+        assert xsh._has_xsh_literal(s) == (xsh._XSH_LITERAL.search(s) is not None), repr(s)
+    for s in ('x = p"/tmp"', "fp'{a}'", 'files = g`*.py`', "help'", "a.p'x'", 'print("p")'):
+        assert xsh._has_xsh_literal(s) == (xsh._XSH_LITERAL.search(s) is not None), s
