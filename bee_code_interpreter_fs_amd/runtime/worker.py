@@ -673,6 +673,8 @@ def _serve(cwd: str, chan: _Chan) -> None:
 
         jail.apply([cwd, os.environ.get("BEE_RUNTIME_PACKAGES", ""), os.environ.get("TMPDIR", ""),
                     os.environ.get("BEE_JAIL_SHARED", "")])
+        if os.environ.get("BEE_FAULT_DIE_WARM") == "1":
+            os._exit(71)  # injected warm-up failure (executor --fault-spawn-fail-rate)
         _cpu_stamp("hello")
         reseed_entropy_state()
         t0 = time.perf_counter()

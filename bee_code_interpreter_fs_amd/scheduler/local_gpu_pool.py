@@ -287,6 +287,7 @@ class LocalGpuPoolBackend(CodeExecutor):
                         "--nano-zygotes", str(c.nano_zygotes_per_gpu),
                         "--nano-cpu-target", str(c.nano_cpu_workers_per_gpu_target),
                         "--gang-grace", str(c.gang_failure_grace_s),
+                        "--fault-spawn-fail-rate", repr(float(c.fault_spawn_fail_rate or 0.0)),
                         "--gang-warm", ";".join(self._gang_keys_led_by(i)),
                         "--gang-env", ",".join(f"{k}={v}" for k, v in sorted((c.gang_rccl_env or {}).items())
                                                if "," not in f"{k}={v}"),
@@ -349,7 +350,8 @@ class LocalGpuPoolBackend(CodeExecutor):
                     # warm gang rank sets (their HIP + torch init is seconds of
                     # CPU per rank: done before READY, not inside the first
                     # requests' window)
-                    and all(v == "ready" for v in (st.get("gang_warm") or {}).values()))
+                    # ("disabled": the set failed to start 3 times; its gangs start cold)
+                    and all(v in ("ready", "disabled") for v in (st.get("gang_warm") or {}).values()))
 
         while loop.time() < deadline:
             try:

@@ -525,6 +525,7 @@ void SandboxPool::zygote_reader(Zygote* z) {
       if (it != workers_.end()) {
         auto w = it->second;
         w->state = WorkerState::Failed;
+        w->died_warming = true;
         w->fail_reason = m["error"].as_string();
         workers_.erase(it);
         release_uid_locked(w);
@@ -555,6 +556,7 @@ void SandboxPool::zygote_reader(Zygote* z) {
         w->state = WorkerState::Exited;
         if (prev == WorkerState::Spawning || prev == WorkerState::Connected) {
           // died before it became ready
+          w->died_warming = true;
           if (w->pooled) spawning_[w->kind]--;
           if (w->kind == kDirect) inflight_spawns_--;
           m_spawn_failed_++;
@@ -798,6 +800,10 @@ std::shared_ptr<Worker> SandboxPool::spawn_worker(bool pooled, int kind, const s
   }
   const bool warm = pooled && kind == kDirect && cfg_.warm_gpu && !gpus.empty();
   if (warm) env.set("BEE_WARM_GPU", "1");
+  // fault injection (config.fault_spawn_fail_rate): off the request path only
+  // -- pooled sandboxes here, warm gang ranks in refill_gangs_locked -- the
+  // sandbox exits during its warm-up, as one whose device or imports failed would
+  if (pooled && fault_spawn_now()) env.set("BEE_FAULT_DIE_WARM", "1");
   if (kind != kDirect && broker_) env.set("BEE_BROKER_SOCK", broker_->socket_path());
   if (kind == kMinCpu || kind == kNanoCpu) env.set("BEE_BROKER_LAZY", "1");
   if (cfg_.default_hbm_quota > 0) env.set("BEE_HBM_QUOTA_BYTES", std::to_string(cfg_.default_hbm_quota));
@@ -888,9 +894,17 @@ void SandboxPool::refill_gangs_locked() {
   for (const auto& key : cfg_.gang_warm) {
     auto it = gang_sets_.find(key);
     if (it != gang_sets_.end()) {
-      bool broken = false;
-      for (auto& w : it->second) broken = broken || w->exited || w->state == WorkerState::Failed;
+      bool broken = false, warm_failure = false, all_ready = true;
+      for (auto& w : it->second) {
+        broken = broken || w->exited || w->state == WorkerState::Failed;
+        warm_failure = warm_failure || w->died_warming || w->state == WorkerState::Failed;
+        all_ready = all_ready && w->state == WorkerState::Ready && !w->exited;
+      }
+      if (all_ready) gang_fails_[key] = 0;
       if (!broken) continue;
+      if (warm_failure && ++gang_fails_[key] == kGangWarmMaxFails)
+        BEE_WARN("warm gang set %s failed to start %d times: its gangs start cold from now on", key.c_str(),
+                 kGangWarmMaxFails);
       for (auto& w : it->second) {  // one rank died while pooled: the set is useless
         if (w->pid > 0) kill(-w->pid, SIGKILL);
         release_uid_locked(w);
@@ -899,12 +913,14 @@ void SandboxPool::refill_gangs_locked() {
       }
       gang_sets_.erase(it);
     }
+    if (gang_fails_[key] >= kGangWarmMaxFails) continue;
     const int n = 1 + (int)std::count(key.begin(), key.end(), ',');
     std::vector<std::shared_ptr<Worker>> set;
     std::string ws0, rp0;
     uid_t uid0 = 0;
     for (int r = 0; r < n; ++r) {
       Json e = gang_rank_env(r, n, cfg_.gang_env);
+      if (fault_spawn_now()) e.set("BEE_FAULT_DIE_WARM", "1");
       if (cfg_.warm_gpu) {
         e.set("BEE_WARM_GPU", "1");
         e.set("BEE_WARM_TORCH", "1");
@@ -934,6 +950,11 @@ std::vector<std::shared_ptr<Worker>> SandboxPool::take_gang_locked(const std::st
   for (auto& w : set) w->state = WorkerState::Running;
   request_refill_locked();
   return set;
+}
+
+bool SandboxPool::fault_spawn_now() const {
+  return cfg_.fault_spawn_fail_rate > 0 &&
+         (double)strtoul(random_hex(3).c_str(), nullptr, 16) / 16777216.0 < cfg_.fault_spawn_fail_rate;
 }
 
 int SandboxPool::target_of(int kind) const {
@@ -2025,14 +2046,17 @@ Json SandboxPool::status() {
   j.set("ready_direct", (int64_t)ready_[kDirect].size());
   j.set("ready_light", (int64_t)ready_[kLight].size());
   {
-    // warm gang sets this daemon leads: "ready" (every rank warm) or "warming"
+    // warm gang sets this daemon leads: "ready" (every rank warm), "warming",
+    // or "disabled" (kGangWarmMaxFails warm-up failures: its gangs start cold)
     Json gw = Json::object();
     for (const auto& key : cfg_.gang_warm) {
       auto it = gang_sets_.find(key);
       bool ready = it != gang_sets_.end();
       if (ready)
         for (auto& w : it->second) ready = ready && w->state == WorkerState::Ready && !w->exited;
-      gw.set(key, ready ? "ready" : "warming");
+      auto f = gang_fails_.find(key);
+      const bool disabled = !ready && f != gang_fails_.end() && f->second >= kGangWarmMaxFails;
+      gw.set(key, ready ? "ready" : disabled ? "disabled" : "warming");
     }
     j.set("gang_warm", gw);
     j.set("gang_warm_hits", (int64_t)m_gang_warm_hits_.load());

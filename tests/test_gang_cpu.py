@@ -168,3 +168,71 @@ def test_cpu_only_pools_take_the_cpu_targets(tmp_path):
     st, body = asyncio.run(go(["--nano-target", "0", "--nano-cpu-target", "2", "--min-target", "0"]))
     assert st["nano_target"] == 2 and st["ready_nano"] == 2 and st["min_target"] == 0, st
     assert body["stdout"] == "6\n"
+
+
+def _metric(text: str, name: str) -> float:
+    return float(next(l for l in text.splitlines() if l.startswith((name + " ", name + "{"))).split()[-1])
+
+
+def test_a_warm_gang_set_that_cannot_start_is_given_up(tmp_path):
+    """Fault injection into the warm gang ranks (every one dies in its
+    warm-up): the daemon re-spawns the set a bounded number of times, then
+    reports it "disabled" (its gangs start cold; the service's start-up wait
+    accepts that) and stops forking torch ranks for it."""
+    ensure_native_executor()
+
+    async def go():
+        ex = ExecutorProcess("gangfail", str(tmp_path / "sb"), gpus="", target=1,
+                             extra_args=["--gang-warm", "0,1", "--gang-env", "BEE_FAULT_DIE_WARM=1"])
+        await ex.start()
+        try:
+            await ex.wait_ready(1, 120)
+            states = []
+            for _ in range(600):
+                st = await ex.get_json("/v1/status")
+                states.append(st["gang_warm"].get("0,1"))
+                if states[-1] == "disabled":
+                    break
+                await asyncio.sleep(0.1)
+            m0 = _metric((await ex.client.request("GET", "/metrics", None, 10)).text,
+                         "bee_executor_worker_spawn_failures_total")
+            await asyncio.sleep(2.0)
+            m1 = _metric((await ex.client.request("GET", "/metrics", None, 10)).text,
+                         "bee_executor_worker_spawn_failures_total")
+            r = await ex.post("/v1/execute", {"source_code": "print(4)"}, timeout=60)
+            return states, m0, m1, r.json()
+        finally:
+            await ex.close()
+
+    states, m0, m1, body = asyncio.run(go())
+    assert states[-1] == "disabled", states[-10:]
+    assert "ready" not in states
+    assert m0 >= 3 and m1 == m0, (m0, m1)  # no more ranks forked once given up
+    assert body["stdout"] == "4\n"  # the rest of the pool is unaffected
+
+
+def test_pooled_spawn_faults_are_absorbed(tmp_path):
+    """--fault-spawn-fail-rate (config.fault_spawn_fail_rate): a share of
+    pooled sandboxes dies in warm-up; the pool refills around them and
+    requests are served."""
+    ensure_native_executor()
+
+    async def go():
+        ex = ExecutorProcess("faults", str(tmp_path / "sb"), gpus="", target=2,
+                             extra_args=["--fault-spawn-fail-rate", "0.5"])
+        await ex.start()
+        try:
+            await ex.wait_ready(1, 120)
+            outs = []
+            for i in range(8):
+                r = await ex.post("/v1/execute", {"source_code": f"print({i})"}, timeout=60)
+                outs.append(r.json()["stdout"])
+            m = _metric((await ex.client.request("GET", "/metrics", None, 10)).text,
+                        "bee_executor_worker_spawn_failures_total")
+            return outs, m
+        finally:
+            await ex.close()
+
+    outs, failures = asyncio.run(go())
+    assert outs == [f"{i}\n" for i in range(8)]
+    assert failures >= 1  # p(no failure in >= 10 spawns at 0.5) < 0.1%
