@@ -36,7 +36,7 @@ NAMES = {0: "round1", 1: "keep_b0", 2: "round1_nostagger", 3: "keep_b0_nostagger
          49: "w4_asm_twobar_g10_ntstore", 50: "w4_asm_twobar_ntstore_edge",
          51: "diag_twobar_no_vmwait", 52: "diag_twobar_no_bar2", 53: "diag_twobar_no_bar1", 54: "diag_twobar_no_syncs",
          55: "diag_twobar_no_next_reads", 56: "diag_twobar_no_glds", 57: "w4_asm_twobar_g10_swapab",
-         58: "w4_asm_twobar_g10_ntstore_reads12"}
+         58: "w4_asm_twobar_g10_ntstore_reads12", 59: "shipped_group2", 60: "shipped_group8", 61: "shipped_group16"}
 DIAG = {4, 5, 25, 28, 32, 33, 34, 36, 38, 40, 42, 51, 52, 53, 54, 55, 56}
 PROD = None
 

@@ -71,7 +71,11 @@ constexpr long long kW4Opts[] = {0, g4::kPinOrder, g4::kInterleave, g4::kNoCarry
                            g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore | g4::kDiagNoReads0,
                            g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore | g4::kDiagNoGlds,
                            g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kSwapAB,
-                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore | g4::kReads12};
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore | g4::kReads12,
+                           // the shipped schedule with the other L2 tile groupings (kGroupM = 4 ships)
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore | g4::kGroup2,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore | g4::kGroup8,
+                           g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore | g4::kGroup16};
 template <int I>
 void run_w4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool bf,
             hipStream_t s) {
@@ -144,6 +148,9 @@ BK_API int gemmlab_run(int variant, const void* A, const void* Bt, void* C, int 
     case 56: run_w4<50>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 57: run_w4<51>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     case 58: run_w4<52>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 59: run_w4<53>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 60: run_w4<54>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
+    case 61: run_w4<55>(A, Bt, C, M, N, K, lda, ldb, ldc, bf, s); break;
     default: return kBadArgument;
   }
   return launch_status();
