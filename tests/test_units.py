@@ -583,3 +583,25 @@ def test_precompile_only_repeated_sources():
     src = "print('precompile-once-%d')\n" % os.getpid()
     assert lgp.precompiled_if_repeated(src) is None  # first sight: the sandbox compiles
     assert lgp.precompiled_if_repeated(src) == lgp.precompiled(src)  # seen before: shipped compiled
+
+
+def test_wait_warm_accepts_a_disabled_warm_gang_set():
+    """A warm gang set the daemon gave up on ("disabled") does not hold the
+    service's READY back; one still "warming" does (until the timeout)."""
+    from types import SimpleNamespace
+
+    from bee_code_interpreter_fs_amd.scheduler.local_gpu_pool import LocalGpuPoolBackend
+
+    def backend(gang_state):
+        st = {"zygotes_alive": 1, "zygotes": 1, "ready_direct": 1, "target": 1, "gang_warm": {"0,1": gang_state}}
+
+        async def get_json(path):
+            return st
+
+        b = LocalGpuPoolBackend.__new__(LocalGpuPoolBackend)
+        b.slots = [SimpleNamespace(executor=SimpleNamespace(get_json=get_json))]
+        return b
+
+    assert asyncio.run(backend("ready").wait_warm(1.0)) is True
+    assert asyncio.run(backend("disabled").wait_warm(1.0)) is True
+    assert asyncio.run(backend("warming").wait_warm(0.3)) is False
