@@ -905,22 +905,26 @@ def main():
                 gc.collect()
                 gc.freeze()  # the clients' heap out of the timed window's collections
             barrier()
-            cpu0, cpu_src = cpu_usage_s()
             thr0 = cpu_throttle()
             roles0 = cpu_by_role(svc_pid)
             threads0 = daemon_threads(svc_pid)
             slots0 = slot_executions(hport) if rank == 0 else None
             trace = [] if os.environ.get("BEE_BENCH_TRACE") else None
+            # the container's CPU counter right around the timed window: the
+            # samplers above and below (/proc walks, a status call through the
+            # front-end) stay out of CPU per Execute
+            cpu0, cpu_src = cpu_usage_s()
             t0 = time.perf_counter()
             lat, errors, exec_times, phases, checks = loop.run_until_complete(
                 run_clients(stubs, source, args.steps, trace, extra=extra))
             barrier()
             elapsed = time.perf_counter() - t0
+            cpu1 = cpu_usage_s()[0]
             thr1 = cpu_throttle()
             roles1 = cpu_by_role(svc_pid)
             threads1 = daemon_threads(svc_pid)
             slots1 = slot_executions(hport) if rank == 0 else None
-            cpu_busy = (cpu_usage_s()[0] - cpu0) / elapsed if elapsed > 0 else 0.0
+            cpu_busy = (cpu1 - cpu0) / elapsed if elapsed > 0 else 0.0
             gathered = [(elapsed, lat, errors, exec_times, phases, checks)]
             if trace is not None:  # completion time (s after t0) and latency of every timed Execute
                 with open(os.environ["BEE_BENCH_TRACE"], "w") as fh:
