@@ -61,7 +61,7 @@ def _targets() -> List[Target]:
         Target(
             name="beekern",
             output=os.path.join(PKG, "ops", "lib", "libbeekern.so"),
-            sources=[os.path.join(k, f) for f in ("random.hip", "elementwise.hip", "reduce.hip", "gemm_bf16.hip", "gemm_bf16_256.hip", "gemm_bf16_256x.hip", "runtime.cpp")],
+            sources=[os.path.join(k, f) for f in ("random.hip", "elementwise.hip", "reduce.hip", "gemm_bf16.hip", "gemm_bf16_256.hip", "gemm_bf16_256x.hip", "gemm_fp.hip", "runtime.cpp")],
             compiler=HIPCC,
             compile_flags=HIP_FLAGS,
             link_flags=[f"--offload-arch={ARCH}", "-shared", "-fPIC"],

@@ -3,7 +3,7 @@
 Exposed to sandboxed code as the top-level module ``beekern`` (see
 ``runtime/sandbox_modules/beekern.py``).  Kernels: Philox RNG, elementwise
 (square & friends), deterministic reductions (sum, fused square-sum, dot,
-min/max), bf16 MFMA GEMM — source in ``csrc/kernels``.
+min/max), bf16 MFMA GEMM and f64 / f32 MFMA GEMM at numpy's precision — source in ``csrc/kernels``.
 """
 
 from ._native import BeekernError, QuotaExceeded, library_path  # noqa: F401
@@ -33,6 +33,7 @@ from .array import (  # noqa: F401
     is_initialized,
     log,
     matmul,
+    matmul_fp,
     max_abs_diff,
     maximum,
     mean,

@@ -535,9 +535,10 @@ def mean(x, axis: Optional[int] = None):
 
 
 def dot(a, b):
-    a, b = _as_operand(a)._materialize(), _as_operand(b)._materialize()
+    a, b = _as_operand(a), _as_operand(b)
     if a.ndim == 2 or b.ndim == 2:
-        return matmul(a, b)
+        return matmul(a, b)  # (.T views stay views: the GEMMs read them in place)
+    a, b = a._materialize(), b._materialize()
     if a.shape != b.shape or a.dtype != b.dtype:
         raise ValueError("dot: 1-D operands must match in shape and dtype")
     return _reduce("dot", a, b)
@@ -607,17 +608,68 @@ def _use_nn(M: int) -> bool:
     return _GEMM_NN == "1" or (_GEMM_NN == "auto" and M < _NN_MAX_M)
 
 
-def matmul(a, b, out_dtype: str = "bfloat16") -> DeviceArray:
-    """C = A @ B on the bf16 MFMA GEMM (f32 accumulate).
+def _fp_dtype(x) -> bool:
+    return x.dtype in ("float32", "float64")
 
-    ``b.T`` views of a row-major [N, K] buffer are used as is (the TN
-    kernels); a plain row-major bf16 ``b`` is read in place by the [K][N]
-    kernel for tile-multiple shapes with M below ~6k (BEE_GEMM_NN), else
-    transposed once on device (15 us at 4096^2) for the TN kernel; an f32/f64
-    ``b`` is converted and transposed in the same pass.
+
+def matmul_fp(a, b) -> DeviceArray:
+    """C = A @ B in numpy's precision: f64 operands on the f64 MFMA
+    (``v_mfma_f64_16x16x4_f64``), f32 on the exact f32 MFMA
+    (``v_mfma_f32_16x16x4_f32``), mixed f32/f64 promoted to f64 as numpy
+    does (``csrc/kernels/gemm_fp.hip``).  numpy's 1-D rules: a 1-D ``a`` is
+    a row vector, a 1-D ``b`` a column, and that axis is dropped from the
+    result.  ``.T`` views are read in place (no transpose pass)."""
+    a = _as_operand(a)
+    b = _as_operand(b)
+    if not (_fp_dtype(a) and _fp_dtype(b)) or a.ndim not in (1, 2) or b.ndim not in (1, 2):
+        raise ValueError(f"matmul_fp: f32/f64 operands of 1 or 2 dimensions, got {a.shape} {a.dtype} @ {b.shape} {b.dtype}")
+    dt = "float64" if "float64" in (a.dtype, b.dtype) else "float32"
+    a1, b1 = a.ndim == 1, b.ndim == 1
+    if a1:
+        a = a.reshape(1, a.shape[0])
+    if b1:
+        b = b.reshape(b.shape[0], 1)
+    if a.shape[1] != b.shape[0]:
+        raise ValueError(f"matmul: incompatible shapes {a.shape} @ {b.shape}")
+    if a.dtype != dt:
+        a = a.astype(dt)
+    if b.dtype != dt:
+        b = b.astype(dt)
+    M, K = a.shape
+    N = b.shape[1]
+    out_shape = tuple(s for s, drop in ((M, a1), (N, b1)) if not drop)
+    if M == 0 or N == 0 or K == 0:
+        return zeros(out_shape, dt)  # (numpy: an empty product, or zeros for K == 0)
+    # a .T view is never lazy (T materialises first): its buffer is the
+    # row-major transpose, read as is with the transposed-operand flag
+    ta, tb = a._transposed, b._transposed
+    a_ptr = a._buf.ptr if ta else a.ptr  # type: ignore[union-attr]
+    b_ptr = b._buf.ptr if tb else b.ptr  # type: ignore[union-attr]
+    c = DeviceArray((M, N), dt)
+    driver().gemm_fp(DTYPE_CODES[dt], ta, tb, a_ptr, b_ptr, c.ptr, M, N, K, M if ta else K, K if tb else N, N)
+    return c.reshape(out_shape) if out_shape != (M, N) else c
+
+
+def matmul(a, b, out_dtype: Optional[str] = None) -> DeviceArray:
+    """C = A @ B.
+
+    f32 / f64 operands (and no ``out_dtype``): numpy's precision on the
+    full-precision MFMA GEMM (:func:`matmul_fp`).  A bf16 operand or an
+    explicit ``out_dtype``: the bf16 MFMA GEMM (f32 accumulate; f32 / f64
+    operands are rounded to bf16), bf16 result by default.
+
+    On the bf16 path ``b.T`` views of a row-major [N, K] buffer are used as
+    is (the TN kernels); a plain row-major bf16 ``b`` is read in place by the
+    [K][N] kernel for tile-multiple shapes with M below ~6k (BEE_GEMM_NN),
+    else transposed once on device (15 us at 4096^2) for the TN kernel; an
+    f32/f64 ``b`` is converted and transposed in the same pass.
     """
     a = _as_operand(a)
     b = _as_operand(b)
+    if out_dtype is None:
+        if _fp_dtype(a) and _fp_dtype(b):
+            return matmul_fp(a, b)
+        out_dtype = "bfloat16"
     if a.ndim != 2 or b.ndim != 2 or a.shape[1] != b.shape[0]:
         raise ValueError(f"matmul: incompatible shapes {a.shape} @ {b.shape}")
     M, K = a.shape

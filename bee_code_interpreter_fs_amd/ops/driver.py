@@ -107,6 +107,12 @@ class NativeDriver:
             "bk_gemm_bf16_nn",
         )
 
+    def gemm_fp(self, dt, ta, tb, A, B, C, M, N, K, lda, ldb, ldc) -> None:
+        """C = op(A) . op(B) in f64 (dt 1) / f32 (dt 0); ta: A given as [K][M],
+        tb: B given as [N][K] (csrc/kernels/gemm_fp.hip)."""
+        check(self.lib.bk_gemm_fp(dt, int(ta), int(tb), _vp(A), _vp(B), _vp(C), M, N, K, lda, ldb, ldc, self.stream),
+              "bk_gemm_fp")
+
     def reduce_axis(self, op: int, dt: int, x: int, y: int, rows: int, cols: int, ld: int, axis: int) -> None:
         if not self.axis_ws:
             self.axis_ws = self.malloc(self.lib.bk_reduce_axis_workspace_bytes())
@@ -172,7 +178,7 @@ def _info_dict(v, arch: str) -> dict:
 # ---- broker client --------------------------------------------------------------------
 
 (HELLO, ALLOC, FREE, WRITE, READ, RAND, UNARY, BINARY, CAST, FILL, REDUCE, GEMM, TRANSPOSE, SYNC, MEMSTATS, INFO,
- COPY, RAND_REDUCE, ALLOC_AT, REDUCE_AXIS) = range(1, 21)
+ COPY, RAND_REDUCE, ALLOC_AT, REDUCE_AXIS, GEMM_FP) = range(1, 22)
 _HDR = struct.Struct("<IIQ")
 _NO_REPLY = 1  # request flag: no response unless a later request collects an error
 _RHDR = struct.Struct("<iIQ")
@@ -400,6 +406,10 @@ class BrokerDriver:
     def gemm_nn(self, A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, odt) -> None:
         # flags bit 0: the second operand is B[K][N] (broker_core.cpp kGemmNN)
         self._post(GEMM, struct.pack("<QQQiiiiiiffii", A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, 1))
+
+    def gemm_fp(self, dt, ta, tb, A, B, C, M, N, K, lda, ldb, ldc) -> None:
+        flags = (1 if ta else 0) | (2 if tb else 0)
+        self._post(GEMM_FP, struct.pack("<IIQQQiiiiqqq", dt, flags, A, B, C, M, N, K, 0, lda, ldb, ldc))
 
     def reduce_axis(self, op, dt, x, y, rows, cols, ld, axis) -> None:
         self._post(REDUCE_AXIS, struct.pack("<IIQQqqqII", op, dt, x, y, rows, cols, ld, axis, 0))

@@ -15,9 +15,13 @@ what numpy would (same dtype rules, same shape):
   ``std`` (two passes, as numpy), ``linalg.norm`` (fused square-sum),
   ``copy`` / ``reshape`` / ``ravel``, and the metadata functions
   ``shape`` / ``ndim`` / ``size``;
-* ``matmul`` / ``dot`` of 2-D operands only when they are bf16 already (the
-  MFMA GEMM rounds f32 / f64 operands to bf16, which numpy would not) --
-  ``BEE_NUMPY_OFFLOAD_MATMUL=bf16`` opts f32 / f64 products into it.
+* ``matmul`` / ``dot`` / ``@`` of 1-D and 2-D operands: f32 / f64 on the
+  full-precision MFMA GEMM in numpy's result dtype (``ops/array.py``
+  ``matmul_fp``, ``csrc/kernels/gemm_fp.hip``; ``.T`` views read in place),
+  bf16 on the bf16 MFMA GEMM.  A host ndarray operand of a product with a
+  device array is uploaded once and the result stays on the device
+  (``BEE_NUMPY_OFFLOAD_MATMUL=bf16`` rounds f32 / f64 products to the bf16
+  GEMM instead, as before).
 
 Everything else copies the operands to the host (``__array__``) and runs
 numpy there, with one ``HostFallbackWarning`` per function per process
@@ -120,10 +124,57 @@ def _any_on_device(b: Binding, objs) -> bool:
     return False
 
 
-def _matmul_gpu_ok(a, c) -> bool:
-    if a.ndim != 2 or c.ndim != 2 or a.shape[1] != c.shape[0] or a.dtype != c.dtype:
-        return False
-    return a.dtype == "bfloat16" or os.environ.get("BEE_NUMPY_OFFLOAD_MATMUL", "") == "bf16"
+_FP = ("float32", "float64")
+
+
+def _matmul(b: Binding, A, x, y, name: str = "matmul"):
+    """The device result of numpy's ``matmul`` / ``dot`` of ``x`` and ``y``
+    (numpy's dtype rules and 1-D semantics), or None for a host fallback.
+
+    One operand may be a host ndarray (or list) when the other is on the
+    device: it is uploaded once -- a product with a device array is worth one
+    host-to-device copy of the other operand -- and the result stays on the
+    device.  N-D (batched) operands, integer results and shape errors go to
+    numpy on the host (which raises numpy's own error for the last)."""
+    dx, dy = b.dev(x), b.dev(y)
+    if dx is None and dy is None:
+        return None
+    if (dx is None and b.is_mine(x)) or (dy is None and b.is_mine(y)):
+        return None  # a host-resident offload array: everything stays on the host
+    if "bfloat16" in (getattr(dx, "dtype", None), getattr(dy, "dtype", None)):
+        if dx is None or dy is None or dx.dtype != dy.dtype or dx.ndim != 2 or dy.ndim != 2 or \
+                dx.shape[1] != dy.shape[0]:
+            return None
+        return A.matmul(dx, dy)
+
+    def np_dtype(obj, d):
+        if d is not None:
+            return np.dtype(d.dtype)
+        h = np.asarray(obj)
+        return h.dtype if h.dtype.kind in "biuf" and h.ndim in (1, 2) and h.size else None
+
+    tx, ty = np_dtype(x, dx), np_dtype(y, dy)
+    if tx is None or ty is None:
+        return None
+    rt = np.result_type(tx, ty)
+    if rt.name not in _FP:
+        return None
+    shapes = [d.shape if d is not None else np.shape(o) for o, d in ((x, dx), (y, dy))]
+    if any(len(s) not in (1, 2) for s in shapes):
+        return None
+    if name == "dot" and len(shapes[0]) == 1 and len(shapes[1]) == 1:
+        return None  # (1-D . 1-D is the reduction path)
+    kx = shapes[0][-1]
+    ky = shapes[1][0]
+    if kx != ky:
+        return None
+    if dx is None:
+        dx = A.asarray(np.asarray(x), rt.name)
+    if dy is None:
+        dy = A.asarray(np.asarray(y), rt.name)
+    if os.environ.get("BEE_NUMPY_OFFLOAD_MATMUL", "") == "bf16" and dx.ndim == 2 and dy.ndim == 2:
+        return A.matmul(dx, dy, out_dtype="float32").astype(rt.name)
+    return A.matmul_fp(dx, dy)
 
 
 def array_ufunc(b: Binding, ufunc, method: str, inputs, kwargs):
@@ -150,6 +201,10 @@ def _try_ufunc(b, A, ufunc, name, method, inputs, kwargs, extra) -> Optional[Any
     if method == "__call__":
         if extra - {"dtype"}:
             return None
+        if name == "matmul":
+            if len(inputs) != 2 or out is not None or kwargs.get("dtype") is not None:
+                return None
+            return _matmul(b, A, inputs[0], inputs[1])
         devs = [b.dev(x) for x in inputs]
         arrays = [d for d in devs if d is not None]
         if not arrays or any(b.is_mine(x) and d is None for x, d in zip(inputs, devs)):
@@ -183,13 +238,6 @@ def _try_ufunc(b, A, ufunc, name, method, inputs, kwargs, extra) -> Optional[Any
             if name == "power" and not rev and float(s) == 2.0:
                 return A.square(arr)
             return A._binary(_BINARY[name], arr, float(s), reversed_=rev)
-        if name == "matmul" and len(inputs) == 2 and all(d is not None for d in devs) and out is None:
-            x, y = devs
-            if not _matmul_gpu_ok(x, y):
-                return None
-            if dt == "bfloat16":
-                return A.matmul(x, y)
-            return A.matmul(x, y, out_dtype="float32").astype(dt)
         return None
     if method == "reduce" and name in _REDUCE and len(inputs) == 1 and out is None:
         if extra - {"axis", "dtype"}:
@@ -302,24 +350,31 @@ def _try_function(b, A, name, mod, args, kwargs):
             return _NO
         return _as_result_scalar(math.sqrt(float(A.square_sum(x))), x.dtype)
     if name in ("dot", "vdot", "inner"):
-        if kwargs or len(args) != 2:
+        if len(args) != 2 or not _kw_only(kwargs, ()):
             return _NO
         x, y = b.dev(args[0]), b.dev(args[1])
-        if x is None or y is None or x.dtype != y.dtype:
-            return _NO
-        if x.ndim == 1 and y.ndim == 1 and x.shape == y.shape:
+        if x is not None and y is not None and x.ndim == 1 and y.ndim == 1 and x.shape == y.shape and \
+                x.dtype == y.dtype:
             return _as_result_scalar(A.dot(x, y), x.dtype)
-        if name == "dot" and _matmul_gpu_ok(x, y):
-            r = A.matmul(x, y) if x.dtype == "bfloat16" else A.matmul(x, y, out_dtype="float32").astype(x.dtype)
-            return b.box(r)
+        if name == "dot":
+            r = _matmul(b, A, args[0], args[1], "dot")
+            return _NO if r is None else b.box(r)
         return _NO
     if name == "copy" and len(args) == 1 and not kwargs:
         x = b.dev(args[0])
         return _NO if x is None else b.box(x.copy())
     if name in ("reshape", "ravel"):
         params = ("a", "shape") if name == "reshape" else ("a",)
-        got = _bind(name, args, kwargs, params + ("order",))
-        if got is None or got.get("order", "C") not in ("C", None):
+        kw = dict(kwargs)
+        if name == "reshape" and "newshape" in kw:  # numpy < 2.1's name, deprecated but still accepted
+            if "shape" in kw or len(args) > 1:
+                return _NO
+            kw["shape"] = kw.pop("newshape")
+        got = _bind(name, args, kw, params + ("order",))
+        # anything else (copy=..., unknown keywords): numpy decides, on the host
+        if got is None or set(got) - set(params) - {"order"} or got.get("order", "C") not in ("C", None):
+            return _NO
+        if name == "reshape" and "shape" not in got:
             return _NO
         x = b.dev(got["a"])
         if x is None:

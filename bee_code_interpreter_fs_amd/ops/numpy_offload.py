@@ -3,8 +3,9 @@
 With offload on (``ExecuteRequest.numpy_offload``, or ``APP_NUMPY_OFFLOAD``
 for every request) the sandbox patches ``numpy.random``'s legacy module
 functions -- ``rand``, ``random`` / ``random_sample`` / ``ranf`` /
-``sample``, ``uniform``, ``randn``, ``standard_normal``, ``normal`` -- so a
-draw of at least ``BEE_NUMPY_OFFLOAD_MIN`` elements (default 2**20) returns
+``sample``, ``uniform``, ``randn``, ``standard_normal``, ``normal`` -- and
+the ``random`` / ``uniform`` / ``normal`` / ``standard_normal`` methods of
+``numpy.random.default_rng()`` Generators, so a draw of at least ``BEE_NUMPY_OFFLOAD_MIN`` elements (default 2**20) returns
 an :class:`OffloadArray`: a device array (Philox4x32-10 on the GPU,
 ``ops/array.py``) that numpy functions and operators dispatch on through
 ``__array_ufunc__`` / ``__array_function__`` (``ops/npinterop.py``).  The
@@ -51,35 +52,78 @@ from ._lazy import np
 MIN_ELEMENTS = int(os.environ.get("BEE_NUMPY_OFFLOAD_MIN", str(1 << 20)) or (1 << 20))
 
 
+class _Residency:
+    """Where one array's data lives: a device array, until the first host
+    operation on it *or on any view of it* moves it to a host ndarray for
+    good.  Views share their base's residency, so they keep aliasing one
+    buffer on either side (a view moved to the host alone used to
+    stop seeing writes through its base)."""
+
+    __slots__ = ("dev", "host")
+
+    def __init__(self, dev, host) -> None:
+        self.dev, self.host = dev, host
+
+    def to_host(self):
+        if self.host is None:
+            self.host = self.dev.numpy()
+            self.dev = None
+        return self.host
+
+
 class OffloadArray:
     """A float64 / float32 numpy-like array resident on the GPU until an
     operation without a kernel moves it to the host for good."""
 
     __array_priority__ = 1000
-    __slots__ = ("_dev", "_host", "__weakref__")
+    __slots__ = ("_res", "_vf", "_dview", "_hview", "__weakref__")
     __hash__ = None  # mutable, like ndarray
 
-    def __init__(self, dev=None, host=None) -> None:
-        object.__setattr__(self, "_dev", dev)
-        object.__setattr__(self, "_host", host)
+    def __init__(self, dev=None, host=None, res=None, vf=None) -> None:
+        # vf: how this view derives from its base (reshape / T), applied to
+        # the device array and to the host ndarray alike
+        res = res if res is not None else _Residency(dev, host)
+        object.__setattr__(self, "_res", res)
+        object.__setattr__(self, "_vf", vf)
+        object.__setattr__(self, "_dview", vf(res.dev) if (vf is not None and res.dev is not None) else None)
+        object.__setattr__(self, "_hview", None)
+
+    def _view(self, fn):
+        """A view of this array sharing its residency (reshape / ravel / T)."""
+        vf = self._vf
+        return OffloadArray(res=self._res, vf=fn if vf is None else (lambda base: fn(vf(base))))
 
     # ---- residency -----------------------------------------------------------------
     @property
+    def _dev(self):
+        r = self._res
+        if r.dev is None:
+            return None
+        return r.dev if self._vf is None else self._dview
+
+    @property
+    def _host(self):
+        return None if self._res.host is None else self._h()
+
+    @property
     def on_device(self) -> bool:
-        return self._dev is not None
+        return self._res.dev is not None
 
     def _h(self):
-        """The host ndarray, downloading (once) and releasing the device copy."""
-        if self._host is None:
-            host = self._dev.numpy()
-            object.__setattr__(self, "_host", host)
-            object.__setattr__(self, "_dev", None)
-        return self._host
+        """The host ndarray, downloading the base (once, for every view of
+        it) and releasing the device copy."""
+        base = self._res.to_host()
+        if self._vf is None:
+            return base
+        if self._hview is None:
+            object.__setattr__(self, "_hview", self._vf(base))
+        return self._hview
 
     # ---- metadata (no transfer) ----------------------------------------------------
     @property
     def shape(self):
-        return self._dev.shape if self._dev is not None else self._host.shape
+        d = self._dev
+        return d.shape if d is not None else self._h().shape
 
     @property
     def ndim(self) -> int:
@@ -87,11 +131,13 @@ class OffloadArray:
 
     @property
     def size(self) -> int:
-        return self._dev.size if self._dev is not None else self._host.size
+        d = self._dev
+        return d.size if d is not None else self._h().size
 
     @property
     def dtype(self):
-        return np.dtype(self._dev.dtype) if self._dev is not None else self._host.dtype
+        d = self._dev
+        return np.dtype(d.dtype) if d is not None else self._h().dtype
 
     @property
     def itemsize(self) -> int:
@@ -112,7 +158,31 @@ class OffloadArray:
         return npinterop.array_ufunc(_BINDING, ufunc, method, inputs, kwargs)
 
     def __array_function__(self, func, types, args, kwargs):
+        v = self._view_function(getattr(func, "__name__", ""), args, kwargs)
+        if v is not None:
+            return v
         return npinterop.array_function(_BINDING, func, types, args, kwargs)
+
+    def _view_function(self, name, args, kwargs):
+        """np.reshape / np.ravel / np.transpose of this device array: a view
+        sharing its residency (not a new array), as numpy returns a view."""
+        if not args or args[0] is not self or not self.on_device:
+            return None
+        kw = {k: v for k, v in kwargs.items() if npinterop._given(v)}
+        if kw.pop("order", "C") not in ("C", None):
+            return None
+        if name == "reshape":
+            if "newshape" in kw and "shape" not in kw:
+                kw["shape"] = kw.pop("newshape")
+            shape = args[1] if len(args) == 2 and "shape" not in kw else kw.pop("shape", None)
+            if shape is None or kw or len(args) > 2:
+                return None
+            return self.reshape(shape)
+        if name == "ravel" and len(args) == 1 and not kw:
+            return self.ravel()
+        if name == "transpose" and len(args) == 1 and not kw.get("axes") and self.ndim == 2:
+            return self.T
+        return None
 
     # ---- reductions and shape methods (device when resident) ------------------------
     def sum(self, axis=None, **kw):
@@ -142,10 +212,18 @@ class OffloadArray:
     def reshape(self, *shape, order="C"):
         if len(shape) == 1 and isinstance(shape[0], (tuple, list)):
             shape = tuple(shape[0])
-        return np.reshape(self, shape, order=order)
+        if self.on_device and order in ("C", None):
+            try:
+                self._dev.reshape(shape)  # (validates the shape; device views share the buffer)
+            except (ValueError, TypeError):
+                return np.reshape(self, shape, order=order)
+            return self._view(lambda base: base.reshape(shape))
+        return self._h().reshape(shape, order=order)
 
     def ravel(self, order="C"):
-        return np.ravel(self, order=order)
+        if self.on_device and order in ("C", None):
+            return self._view(lambda base: base.reshape(-1))
+        return self._h().ravel(order)
 
     def astype(self, dtype, *args, **kwargs):
         dt = np.dtype(dtype)
@@ -160,9 +238,9 @@ class OffloadArray:
 
     def __getattr__(self, name):
         # anything else an ndarray has: on the host copy
-        if name.startswith("__") or name in ("_dev", "_host"):
+        if name.startswith("__") or name in ("_res", "_vf", "_dview", "_hview"):
             raise AttributeError(name)
-        if self._dev is not None:
+        if self.on_device:
             npinterop.warn_fallback(f"ndarray.{name}")
         return getattr(self._h(), name)
 
@@ -257,8 +335,8 @@ class OffloadArray:
 
     @property
     def T(self):
-        if self._dev is not None and self.ndim == 2:
-            return OffloadArray(self._dev.T)
+        if self.on_device and self.ndim == 2:
+            return self._view(lambda base: base.T)
         return self._h().T
 
 
@@ -394,6 +472,69 @@ def _wrap_seed(orig):
     return seed
 
 
+def _generator_class():
+    """numpy.random.Generator with its large float draws on the device: what
+    the patched ``default_rng`` returns.  A subclass, so ``isinstance(rng,
+    np.random.Generator)`` (scipy's ``check_random_state`` and the like)
+    holds, and every method without a device kernel (integers, choice,
+    shuffle, ...) is numpy's own on the same bit generator."""
+    if _GENCLS:
+        return _GENCLS[0]
+
+    class Generator(np.random.Generator):
+        def __init__(self, bit_generator):
+            super().__init__(bit_generator)
+            from .array import Generator as DeviceGenerator
+
+            # the device stream is keyed by the seed sequence: default_rng(s)
+            # twice gives the same device draws (Philox, not PCG64's stream)
+            state = bit_generator.seed_seq.generate_state(2, np.uint64) if hasattr(bit_generator, "seed_seq") \
+                else np.frombuffer(os.urandom(16), np.uint64)
+            self._bee_dev = DeviceGenerator(int(state[0]) ^ (int(state[1]) << 1))
+
+        def _ok(self, size, dtype=np.float64, out=None):
+            return out is None and _big(size) and np.dtype(dtype).name in ("float32", "float64")
+
+        def random(self, size=None, dtype=np.float64, out=None):
+            if self._ok(size, dtype, out):
+                return OffloadArray(self._bee_dev.uniform(0.0, 1.0, _shape(size), np.dtype(dtype).name))
+            return super().random(size, dtype, out)
+
+        def uniform(self, low=0.0, high=1.0, size=None):
+            if self._ok(size) and _scalar(low) and _scalar(high) and math.isfinite(float(low)) and \
+                    math.isfinite(float(high)):
+                return OffloadArray(self._bee_dev.uniform(float(low), float(high), _shape(size)))
+            return super().uniform(low, high, size)
+
+        def standard_normal(self, size=None, dtype=np.float64, out=None):
+            if self._ok(size, dtype, out):
+                return OffloadArray(self._bee_dev.normal(0.0, 1.0, _shape(size), np.dtype(dtype).name))
+            return super().standard_normal(size, dtype, out)
+
+        def normal(self, loc=0.0, scale=1.0, size=None):
+            if self._ok(size) and _scalar(loc) and _scalar(scale) and float(scale) >= 0.0 and math.isfinite(float(loc)):
+                return OffloadArray(self._bee_dev.normal(float(loc), float(scale), _shape(size)))
+            return super().normal(loc, scale, size)
+
+    Generator.__module__ = "numpy.random"
+    _GENCLS.append(Generator)
+    return Generator
+
+
+_GENCLS: list = []
+
+
+def _wrap_default_rng(orig):
+    @functools.wraps(orig)
+    def default_rng(seed=None):
+        rng = orig(seed)
+        if seed is not None and isinstance(seed, np.random.Generator):
+            return rng  # numpy returns a Generator passed in unaltered
+        return _generator_class()(rng.bit_generator)
+
+    return default_rng
+
+
 _WRAPPERS = {
     "rand": _wrap_rand,
     "randn": _wrap_randn,
@@ -405,6 +546,7 @@ _WRAPPERS = {
     "normal": _wrap_normal,
     "standard_normal": _wrap_standard_normal,
     "seed": _wrap_seed,
+    "default_rng": _wrap_default_rng,
 }
 
 

@@ -64,6 +64,7 @@ class HipDevice final : public broker::Device {
     int (*ws_init)(void*, hipStream_t);       // zero a fresh workspace's completion tickets
     int (*axis_ws_init)(void*, hipStream_t);
     int (*reduce_axis)(int, int, const void*, int64_t, int64_t, int64_t, int, void*, void*, hipStream_t);
+    int (*gemm_fp)(int, int, int, const void*, const void*, void*, int, int, int, int64_t, int64_t, int64_t, hipStream_t);
   } bk{};
 
   // Per-session GPU resources, pooled across sessions: a stream, the
@@ -173,6 +174,7 @@ class HipDevice final : public broker::Device {
     }
     sym(lib_, "bk_reduce_axis", &bk.reduce_axis);
     sym(lib_, "bk_gemm_bf16_nn", &bk.gemm_nn);
+    sym(lib_, "bk_gemm_fp", &bk.gemm_fp);
     return true;
   }
 
@@ -371,6 +373,11 @@ class HipDevice final : public broker::Device {
               float beta, int odt, void* s) override {
     if (!bk.gemm_nn) return broker::kBadArgument;
     return bk.gemm_nn(A, B, C, M, N, K, lda, ldb, ldc, alpha, beta, odt, pick(s, short_gemm(M, N, K)));
+  }
+  int gemm_fp(uint32_t dt, bool ta, bool tb, const void* A, const void* B, void* C, int M, int N, int K, int64_t lda,
+              int64_t ldb, int64_t ldc, void* s) override {
+    if (!bk.gemm_fp) return broker::kBadArgument;
+    return bk.gemm_fp((int)dt, ta, tb, A, B, C, M, N, K, lda, ldb, ldc, pick(s, short_gemm(M, N, K)));
   }
   int transpose(int sdt, int ddt, const void* in, void* out, int rows, int cols, int ldi, int ldo, void* s) override {
     return bk.transpose(sdt, ddt, in, out, rows, cols, ldi, ldo,

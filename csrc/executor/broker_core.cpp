@@ -15,7 +15,7 @@ const char* op_name(uint32_t op) {
                                       "bk.read",     "bk.rand",  "bk.unary",  "bk.binary",    "bk.cast",
                                       "bk.fill",     "bk.reduce", "bk.gemm",  "bk.transpose", "bk.sync",
                                       "bk.memstats", "bk.info",  "bk.copy",   "bk.rand_reduce", "bk.alloc_at",
-                                      "bk.reduce_axis"};
+                                      "bk.reduce_axis", "bk.gemm_fp"};
   return op < sizeof(names) / sizeof(names[0]) ? names[op] : names[0];
 }
 
@@ -349,6 +349,26 @@ int32_t Session::dispatch(uint32_t op, const char* payload, uint64_t len, std::v
       if (!will_read(ba) || !will_read(bb) || !(c_full ? will_write(bc, 0, nc) : will_read(bc))) return kLaunchFailed;
       if (nn) return dev_.gemm_nn(ba->ptr, bb->ptr, bc->ptr, M, N, K, lda, ldb, ldc, alpha, beta, odt, stream_);
       return dev_.gemm(ba->ptr, bb->ptr, bc->ptr, M, N, K, lda, ldb, ldc, alpha, beta, odt, stream_);
+    }
+    case kGemmFp: {  // f64 / f32 product, either operand possibly a transposed view
+      const uint32_t dt = r.get<uint32_t>(), gflags = r.get<uint32_t>();
+      const uint64_t A = r.get<uint64_t>(), B = r.get<uint64_t>(), C = r.get<uint64_t>();
+      const int32_t M = r.get<int32_t>(), N = r.get<int32_t>(), K = r.get<int32_t>();
+      (void)r.get<int32_t>();
+      const int64_t lda = r.get<int64_t>(), ldb = r.get<int64_t>(), ldc = r.get<int64_t>();
+      if (!r.ok) return kProtocol;
+      const bool ta = (gflags & 1) != 0, tb = (gflags & 2) != 0;
+      uint64_t na, nb, nc;
+      Buf *ba = lookup(A), *bb = lookup(B), *bc = lookup(C);
+      if ((dt != 0 && dt != 1) || (gflags & ~3u) != 0 ||
+          !(ta ? matrix_bytes(K, M, lda, dtype_size(dt), &na) : matrix_bytes(M, K, lda, dtype_size(dt), &na)) ||
+          !(tb ? matrix_bytes(N, K, ldb, dtype_size(dt), &nb) : matrix_bytes(K, N, ldb, dtype_size(dt), &nb)) ||
+          !matrix_bytes(M, N, ldc, dtype_size(dt), &nc) || !ba || !bb || !bc || na > ba->size || nb > bb->size ||
+          nc > bc->size)
+        return kBadHandle;
+      // C is only written: its untouched gaps (ldc > N) keep their scrub state
+      if (!will_read(ba) || !will_read(bb) || !(ldc == N ? will_write(bc, 0, nc) : will_read(bc))) return kLaunchFailed;
+      return dev_.gemm_fp(dt, ta, tb, ba->ptr, bb->ptr, bc->ptr, M, N, K, lda, ldb, ldc, stream_);
     }
     case kTranspose: {
       const uint64_t in = r.get<uint64_t>(), o = r.get<uint64_t>();

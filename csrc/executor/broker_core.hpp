@@ -25,7 +25,7 @@ namespace broker {
 
 enum Op : uint32_t {
   kHello = 1, kAlloc, kFree, kWrite, kRead, kRand, kUnary, kBinary, kCast, kFill, kReduce, kGemm, kTranspose,
-  kSync, kMemStats, kInfo, kCopy, kRandReduce, kAllocAt, kReduceAxis,
+  kSync, kMemStats, kInfo, kCopy, kRandReduce, kAllocAt, kReduceAxis, kGemmFp,
   kOpCount
 };
 enum Status : int32_t {
@@ -89,6 +89,12 @@ class Device {
   // C = A . B with B stored [K][N]; kBadArgument where the device has no such
   // kernel for the shape (the client then transposes and uses gemm)
   virtual int gemm_nn(const void*, const void*, void*, int, int, int, int, int, int, float, float, int, void*) {
+    return kBadArgument;
+  }
+  // C = op(A) . op(B) in f64 / f32 (bk_gemm_fp): trans_a -> A given as [K][M],
+  // trans_b -> B given as [N][K]; kBadArgument where the device has no such kernel
+  virtual int gemm_fp(uint32_t dt, bool trans_a, bool trans_b, const void*, const void*, void*, int, int, int, int64_t,
+                      int64_t, int64_t, void*) {
     return kBadArgument;
   }
   virtual int transpose(int sdt, int ddt, const void* in, void* out, int rows, int cols, int ldi, int ldo, void* s) = 0;

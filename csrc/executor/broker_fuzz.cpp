@@ -134,6 +134,15 @@ class HostDevice final : public Device {
     }
     return 0;
   }
+  int gemm_fp(uint32_t dt, bool ta, bool tb, const void* A, const void* B, void* C, int M, int N, int K, int64_t lda,
+              int64_t ldb, int64_t ldc, void*) override {
+    const uint64_t es = dtype_size(dt);
+    const int ar = ta ? K : M, ac = ta ? M : K, br = tb ? N : K, bc = tb ? K : N;
+    for (int i = 0; i < ar; ++i) sum((const char*)A + (uint64_t)i * lda * es, (uint64_t)ac * es);
+    for (int i = 0; i < br; ++i) sum((const char*)B + (uint64_t)i * ldb * es, (uint64_t)bc * es);
+    for (int i = 0; i < M; ++i) touch_w((char*)C + (uint64_t)i * ldc * es, (uint64_t)N * es, 0);
+    return 0;
+  }
   int transpose(int sdt, int ddt, const void* in, void* out, int rows, int cols, int ldi, int ldo, void*) override {
     const uint64_t si = dtype_size((uint32_t)sdt), so = dtype_size((uint32_t)ddt);
     for (int i = 0; i < rows; ++i) sum((const char*)in + (uint64_t)i * ldi * si, (uint64_t)cols * si);

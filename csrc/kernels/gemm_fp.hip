@@ -1,0 +1,322 @@
+// Full-precision GEMM for numpy's own dtypes: C = op(A) . op(B) in f64 on
+// v_mfma_f64_16x16x4_f64 and in f32 on v_mfma_f32_16x16x4_f32 (gfx950).
+//
+// Why this kernel exists: the reference's payloads are plain f64 numpy
+// (/root/reference/examples/benchmark-numpy.py:18-22, using_imports.py:20-36);
+// the bf16 MFMA GEMM (gemm_bf16.hip) would round them, which numpy never
+// does.  Both MFMAs here are exact in their dtype: each is a k-ordered
+// chain of fused multiply-adds with one rounding per product (f32: bitwise
+// an fmaf chain, cdna_hip_programming.md §3 "FP32-input MFMA"), so the error
+// against an fp64 reference is that of a blocked dot product in the dtype.
+//
+// Hardware budget (MI355X_MICROARCH.md, Matrix cores): the f64 MFMA issues one
+// 16x16x4 product (2048 flop) per 64 cycles per SIMD and the f32 one per 32
+// cycles -- 78.6 / 157.3 TFLOP/s dense over 256 CUs.  Both are slow next to
+// the LDS and L2, so the design goal is simply to keep every SIMD issuing
+// MFMAs back to back:
+//
+//  * workgroup tile 128x128, 4 waves of 64x64; each wave holds 4x4
+//    accumulators of 16x16 (f64: 128 VGPRs, f32: 64), so one k-step of 4
+//    needs 4 A + 4 B one-element fragment reads for 16 MFMAs (1024 / 512
+//    cycles of MFMA per 8 ds_read);
+//  * K tile of 128 bytes per row (16 f64 / 32 f32): 16 KiB per operand, two
+//    LDS stages per operand = 72 KiB, so two workgroups share a CU and one's
+//    barrier hides behind the other's MFMAs;
+//  * global -> registers -> LDS, one barrier per K tile: the next tile's
+//    16-B loads are in flight during the current tile's MFMAs;
+//  * LDS holds each operand tile in its global orientation (rows copied as
+//    16-B chunks), padded so the fragment reads are bank-conflict free in
+//    either orientation -- so A^T / B^T views (numpy's a.T, e.g. np.dot(a.T,
+//    a)) are read in place, no transpose pass;
+//  * XCD-aware tile order: blocks land on XCD b % 8, so each XCD gets a
+//    contiguous run of tiles, walked in groups of 8 tile rows (the A row
+//    panels and B column panels a group shares stay in that XCD's L2).
+//
+// Any M, N, K and leading dimensions: out-of-range elements load as zero and
+// stores are masked; 16-B loads where pointers and leading dimensions allow,
+// element loads otherwise.
+#include "bk_common.hpp"
+
+namespace bk {
+namespace fp {
+
+constexpr int kBM = 128, kBN = 128, kThreads = 256;
+constexpr int kPitchMN = 128 + 16;  // LDS row of an [k][m|n] tile: 144 elements
+
+template <typename T>
+struct Cfg;
+// K tile = 128 B per row; an [m|n][k] LDS row is padded by 16 B so a
+// fragment read (16 rows x 4 k) hits 64 distinct banks
+template <>
+struct Cfg<double> {
+  static constexpr int BK = 16, kPitchK = 18;
+};
+template <>
+struct Cfg<float> {
+  static constexpr int BK = 32, kPitchK = 36;
+};
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <typename T>
+using acc_t = typename std::conditional<std::is_same<T, double>::value, f64x4, f32x4>::type;
+
+__device__ __forceinline__ f64x4 mfma(double a, double b, f64x4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Accumulator element r of lane l -> (row, col) in the 16x16 tile.  The f64
+// MFMA has its own C/D map (cdna_hip_programming.md §3, Fragment layout):
+// the f32 row formula on it puts 3 of every 4 results in the wrong row.
+template <typename T>
+__device__ __forceinline__ int acc_row(int lane, int r) {
+  if constexpr (std::is_same<T, double>::value)
+    return (lane >> 4) + 4 * r;
+  else
+    return (lane >> 4) * 4 + r;
+}
+
+// One operand tile: `ROWS` x `COLS` elements of a row-major buffer starting
+// at (r0, c0), copied to LDS in the same orientation as 16-B chunks (LDS row
+// pitch PITCH elements).  An A tile is 128 x BK ([m][k]) or BK x 128
+// ([k][m]); a B tile BK x BN or BN x BK.  Chunks are spread evenly over the
+// 256 threads (consecutive threads take consecutive chunks of a row: every
+// 16-B load of a wave lands in whole 64-B segments).
+template <typename T, bool VEC, int ROWS, int COLS, int PITCH>
+struct Tile {
+  static constexpr int E = 16 / sizeof(T);  // elements per 16-B chunk
+  static constexpr int CPR = COLS / E;      // chunks per tile row
+  static constexpr int kChunks = ROWS * CPR / kThreads;
+  static_assert(ROWS * CPR % kThreads == 0, "whole chunks per thread");
+  static constexpr int kLdsElems = ROWS * PITCH;
+  T v[kChunks][E];
+
+  // every element in range (an interior tile): 16-B loads, no guards
+  __device__ __forceinline__ void load_fast(const T* __restrict__ g, int64_t ld, int r0, int c0) {
+    const T* base = g + (int64_t)r0 * ld + c0;
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) {
+      const int q = c * kThreads + (int)threadIdx.x;
+      const u32x4_t w = *reinterpret_cast<const u32x4_t*>(base + (int64_t)(q / CPR) * ld + (q % CPR) * E);
+      __builtin_memcpy(v[c], &w, 16);
+    }
+  }
+
+  // edge tiles: out-of-range elements are zero
+  __device__ __forceinline__ void load_guarded(const T* __restrict__ g, int64_t ld, int row_end, int col_end, int r0,
+                                               int c0) {
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) {
+      const int q = c * kThreads + (int)threadIdx.x;
+      const int row = r0 + q / CPR, col = c0 + (q % CPR) * E;
+      const T* p = g + (int64_t)row * ld + col;
+      if (VEC && row < row_end && col + E <= col_end) {
+        const u32x4_t w = *reinterpret_cast<const u32x4_t*>(p);
+        __builtin_memcpy(v[c], &w, 16);
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[c][e] = (row < row_end && col + e < col_end) ? p[e] : T(0);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(T* lds) const {
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) {
+      const int q = c * kThreads + (int)threadIdx.x;
+      u32x4_t w;
+      __builtin_memcpy(&w, v[c], 16);
+      *reinterpret_cast<u32x4_t*>(lds + (q / CPR) * PITCH + (q % CPR) * E) = w;
+    }
+  }
+};
+
+// C[M][N] = A . B, A[m][k] at a[TA ? k*lda + m : m*lda + k], B[k][n] at
+// b[TB ? n*ldb + k : k*ldb + n].  Workgroup tile 128 x BN (BN = 128, or 64
+// when 128^2 tiles would leave CUs with a single workgroup); 4 waves of
+// 64 x BN/2.
+template <typename T, bool TA, bool TB, bool VEC, int BN>
+__global__ __launch_bounds__(kThreads, 2) void gemm_fp_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                               T* __restrict__ c, int M, int N, int K, int64_t lda,
+                                                               int64_t ldb, int64_t ldc) {
+  constexpr int BK = Cfg<T>::BK, PK = Cfg<T>::kPitchK;
+  constexpr int kPitchN = BN + 16;  // a [k][n] row: f64 = 32, f32 = 16 dwords mod 64 banks
+  constexpr int WN = BN / 2, NT = WN / 16;  // wave columns, 16-wide MFMA tiles per wave row
+  // A tile: [m][k] (row-major A) or [k][m] (A^T view); B tile: [k][n] or [n][k]
+  using TileA = typename std::conditional<TA, Tile<T, VEC, BK, kBM, kPitchMN>, Tile<T, VEC, kBM, BK, PK>>::type;
+  using TileB = typename std::conditional<TB, Tile<T, VEC, BN, BK, PK>, Tile<T, VEC, BK, BN, kPitchN>>::type;
+  __shared__ __attribute__((aligned(16))) T lds_a[2][TileA::kLdsElems];
+  __shared__ __attribute__((aligned(16))) T lds_b[2][TileB::kLdsElems];
+
+  // ---- tile of this block (XCD-aware, grouped) ----
+  const int tiles_m = (M + kBM - 1) / kBM, tiles_n = (N + BN - 1) / BN;
+  const int total = tiles_m * tiles_n;
+  int bid = (int)blockIdx.x;
+  if (total % kNumXCD == 0) bid = (bid % kNumXCD) * (total / kNumXCD) + bid / kNumXCD;
+  constexpr int kGroup = 8;
+  const int per_group = kGroup * tiles_n;
+  const int first_m = (bid / per_group) * kGroup;
+  const int gsz = min(tiles_m - first_m, kGroup);
+  const int tm = first_m + (bid % per_group) % gsz, tn = (bid % per_group) / gsz;
+  const int m0 = tm * kBM, n0 = tn * BN;
+  const bool interior = VEC && m0 + kBM <= M && n0 + BN <= N;  // (uniform)
+
+  const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * WN;
+  const int fr = lane & 15, fk = lane >> 4;  // fragment: row/col within 16, k within 4
+
+  acc_t<T> acc[4][NT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = acc_t<T>{0, 0, 0, 0};
+
+  TileA ta;
+  TileB tb;
+  auto load = [&](int k0) {
+    if (interior && k0 + BK <= K) {
+      if constexpr (TA)
+        ta.load_fast(a, lda, k0, m0);
+      else
+        ta.load_fast(a, lda, m0, k0);
+      if constexpr (TB)
+        tb.load_fast(b, ldb, n0, k0);
+      else
+        tb.load_fast(b, ldb, k0, n0);
+    } else {
+      if constexpr (TA)
+        ta.load_guarded(a, lda, K, M, k0, m0);
+      else
+        ta.load_guarded(a, lda, M, K, m0, k0);
+      if constexpr (TB)
+        tb.load_guarded(b, ldb, N, K, n0, k0);
+      else
+        tb.load_guarded(b, ldb, K, N, k0, n0);
+    }
+  };
+
+  const int nk = (K + BK - 1) / BK;
+  load(0);
+  ta.store(lds_a[0]);
+  tb.store(lds_b[0]);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const T* As = lds_a[cur];
+    const T* Bs = lds_b[cur];
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      T fa[4], fb[NT];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = wm + i * 16 + fr, k = kk + fk;
+        fa[i] = TA ? As[k * kPitchMN + m] : As[m * PK + k];
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = wn + j * 16 + fr, k = kk + fk;
+        fb[j] = TB ? Bs[n * PK + k] : Bs[k * kPitchN + n];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
+      // the next tile's loads go out behind the first k-step's MFMAs, so
+      // this tile's first fragment reads are not queued behind them
+      if (kk == 0 && kt + 1 < nk) load((kt + 1) * BK);
+    }
+    if (kt + 1 < nk) {
+      // the other stage was last read before the previous barrier
+      ta.store(lds_a[cur ^ 1]);
+      tb.store(lds_b[cur ^ 1]);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: lanes 0..15 of a row are 16 consecutive columns ----
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm + i * 16 + acc_row<T>(lane, r);
+      if (m >= M) continue;
+      T* crow = c + (int64_t)m * ldc;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = n0 + wn + j * 16 + fr;
+        if (n < N) crow[n] = acc[i][j][r];
+      }
+    }
+  }
+}
+
+// 128 x 64 tiles when 128 x 128 ones would give fewer than two workgroups
+// per CU (each CU then keeps two resident: one's barrier and fragment-read
+// latency hide behind the other's MFMAs)
+inline bool narrow_tiles(int M, int N) {
+  const int64_t t128 = (int64_t)((M + kBM - 1) / kBM) * ((N + 127) / 128);
+  return t128 < 2 * kNumCU && N > 64;
+}
+
+template <typename T, bool TA, bool TB>
+void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, bool vec,
+            hipStream_t stream) {
+  const bool nar = getenv("BK_GEMM_FP_BN") ? atoi(getenv("BK_GEMM_FP_BN")) == 64 : narrow_tiles(M, N);
+  const int bn = nar ? 64 : 128;
+  const unsigned grid = (unsigned)(((M + kBM - 1) / kBM) * ((N + bn - 1) / bn));
+#define BK_FP_LAUNCH(V, W)                                                                                       \
+  gemm_fp_kernel<T, TA, TB, V, W><<<grid, kThreads, 0, stream>>>((const T*)A, (const T*)B, (T*)C, M, N, K, lda, \
+                                                                 ldb, ldc)
+  if (vec && nar)
+    BK_FP_LAUNCH(true, 64);
+  else if (vec)
+    BK_FP_LAUNCH(true, 128);
+  else if (nar)
+    BK_FP_LAUNCH(false, 64);
+  else
+    BK_FP_LAUNCH(false, 128);
+#undef BK_FP_LAUNCH
+}
+
+template <typename T>
+void dispatch(bool ta, bool tb, const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb,
+              int64_t ldc, bool vec, hipStream_t s) {
+  if (ta && tb)
+    launch<T, true, true>(A, B, C, M, N, K, lda, ldb, ldc, vec, s);
+  else if (ta)
+    launch<T, true, false>(A, B, C, M, N, K, lda, ldb, ldc, vec, s);
+  else if (tb)
+    launch<T, false, true>(A, B, C, M, N, K, lda, ldb, ldc, vec, s);
+  else
+    launch<T, false, false>(A, B, C, M, N, K, lda, ldb, ldc, vec, s);
+}
+
+}  // namespace fp
+}  // namespace bk
+
+using namespace bk;
+
+// C[M][N] = op(A) . op(B) in f64 (dtype kF64) or f32 (kF32), row-major C with
+// leading dimension ldc.  trans_a: A is given as its transpose, a [K][M]
+// buffer (lda >= M); else [M][K] (lda >= K).  trans_b: B given as a [N][K]
+// buffer (ldb >= K); else [K][N] (ldb >= N).  Never reads C.
+BK_API int bk_gemm_fp(int dtype, int trans_a, int trans_b, const void* A, const void* B, void* C, int M, int N, int K,
+                      int64_t lda, int64_t ldb, int64_t ldc, hipStream_t stream) {
+  if (dtype != kF64 && dtype != kF32) return kBadArgument;
+  if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0) return kBadArgument;
+  if (lda < (trans_a ? M : K) || ldb < (trans_b ? K : N) || ldc < N) return kBadArgument;
+  const int64_t tiles = (int64_t)((M + fp::kBM - 1) / fp::kBM) * ((N + 63) / 64);  // (narrow tiles: 64 wide)
+  if (tiles > 0x7fffffffll) return kBadArgument;
+  const int es = dtype_size(dtype);
+  const int e = 16 / es;
+  const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % e == 0 && ldb % e == 0;
+  if (dtype == kF64)
+    fp::dispatch<double>(trans_a != 0, trans_b != 0, A, B, C, M, N, K, lda, ldb, ldc, vec, stream);
+  else
+    fp::dispatch<float>(trans_a != 0, trans_b != 0, A, B, C, M, N, K, lda, ldb, ldc, vec, stream);
+  return launch_status();
+}

@@ -101,7 +101,7 @@ class HostDriver:
             if dt == 1:
                 return uniform_f64(n, seed, off, a, b)
             return uniform_f32(n, seed, off, a, b).astype(np.float64)
-        rng = np.random.default_rng([seed & 0xFFFFFFFFFFFFFFFF, off])
+        rng = np.random.Generator(np.random.PCG64([seed & 0xFFFFFFFFFFFFFFFF, off]))  # (default_rng may be patched)
         return rng.normal(a, b, n)
 
     def rand(self, kind, h, n, dt, seed, off, a, b) -> None:
@@ -184,6 +184,18 @@ class HostDriver:
         a = self._load(A, M * lda, 2).reshape(M, lda)[:, :K]
         b = self._load(B, K * ldb, 2).reshape(K, ldb)[:, :N]
         self._gemm_out(a @ b, C, M, N, ldc, alpha, beta, odt)
+
+    def gemm_fp(self, dt, ta, tb, A, B, C, M, N, K, lda, ldb, ldc) -> None:
+        self.launches.append(("gemm_fp", dt, M, N, K, bool(ta), bool(tb)))
+        a = self._load(A, (K if ta else M) * lda, dt).reshape(-1, lda)[:, : (M if ta else K)]
+        b = self._load(B, (N if tb else K) * ldb, dt).reshape(-1, ldb)[:, : (K if tb else N)]
+        a = a.T if ta else a
+        b = b.T if tb else b
+        np_dt = _NP[dt]
+        prod = a.astype(np_dt) @ b.astype(np_dt)  # numpy's own product in the dtype
+        c = self._load(C, M * ldc, dt).reshape(M, ldc)
+        c[:, :N] = prod
+        self._store(C, c.ravel(), dt)
 
     def _gemm_out(self, prod, C, M, N, ldc, alpha, beta, odt):
         c = self._load(C, M * ldc, odt).reshape(M, ldc)

@@ -1,0 +1,108 @@
+"""The f64 / f32 MFMA GEMM (csrc/kernels/gemm_fp.hip) against fp64 numpy.
+
+numpy's own matmul precision is the contract: an f64 product may differ
+from the fp64 reference only by the rounding of a blocked dot product
+(relative error <= 1e-12 * sqrt(K) of the magnitude scale |A|.|B|), an f32
+product by f32 rounding (<= 1e-5).  Every transpose combination is a
+``.T`` view read in place; ragged shapes, unaligned leading dimensions,
+vectors and NaNs are covered."""
+
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(c, a64, b64, dtype):
+    ref = a64 @ b64
+    scale = np.abs(a64) @ np.abs(b64)
+    err = np.abs(c.astype(np.float64) - ref) / np.maximum(scale, 1e-300)
+    K = a64.shape[-1]
+    tol = 1e-12 * math.sqrt(K) if dtype == "float64" else 1e-5
+    assert float(err.max()) <= tol, (float(err.max()), tol)
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 16), (256, 384, 512), (1000, 777, 333), (1, 513, 64), (513, 1, 64),
+                                   (64, 64, 1), (129, 127, 17), (2048, 2048, 2048)])
+def test_gemm_fp_matches_fp64(gpu, dtype, M, N, K):
+    rng = np.random.default_rng(M * 7 + N * 3 + K)
+    a_h = rng.standard_normal((M, K)).astype(dtype)
+    b_h = rng.standard_normal((K, N)).astype(dtype)
+    c = gpu.matmul(gpu.asarray(a_h), gpu.asarray(b_h))
+    assert c.dtype == dtype and c.shape == (M, N)
+    _check(c.numpy(), a_h.astype(np.float64), b_h.astype(np.float64), dtype)
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+@pytest.mark.parametrize("ta,tb", [(True, False), (False, True), (True, True)])
+def test_gemm_fp_transposed_views(gpu, dtype, ta, tb):
+    """np.dot(a.T, b) and friends: the view's buffer is read in place."""
+    M, N, K = 300, 200, 260
+    rng = np.random.default_rng(11)
+    a_h = rng.standard_normal((K, M) if ta else (M, K)).astype(dtype)
+    b_h = rng.standard_normal((N, K) if tb else (K, N)).astype(dtype)
+    a, b = gpu.asarray(a_h), gpu.asarray(b_h)
+    c = gpu.matmul(a.T if ta else a, b.T if tb else b).numpy()
+    a64 = a_h.astype(np.float64)
+    b64 = b_h.astype(np.float64)
+    _check(c, a64.T if ta else a64, b64.T if tb else b64, dtype)
+
+
+def test_gemm_fp_unaligned_leading_dimensions(gpu):
+    """Leading dimensions that are not a 16-B multiple take the element-load
+    path; a sub-matrix of a wider buffer (lda > K) is read in place."""
+    from bee_code_interpreter_fs_amd.ops import _native
+    from bee_code_interpreter_fs_amd.ops.array import DeviceArray, driver
+
+    M, N, K, lda, ldb, ldc = 131, 67, 45, 47, 69, 71
+    rng = np.random.default_rng(5)
+    A = rng.standard_normal((M, lda))
+    B = rng.standard_normal((K, ldb))
+    a, b = gpu.asarray(A), gpu.asarray(B)
+    c = DeviceArray((M, ldc), "float64")
+    gpu.zeros(1)  # (driver initialised)
+    driver().gemm_fp(_native.DTYPE_CODES["float64"], False, False, a.ptr, b.ptr, c.ptr, M, N, K, lda, ldb, ldc)
+    _check(c.numpy()[:, :N], A[:, :K], B[:, :N], "float64")
+
+
+def test_gemm_fp_propagates_nan_and_inf(gpu):
+    a_h = np.ones((128, 64))
+    b_h = np.ones((64, 128))
+    a_h[3, 5] = np.nan
+    b_h[7, 9] = np.inf
+    c = gpu.matmul(gpu.asarray(a_h), gpu.asarray(b_h)).numpy()
+    want = a_h @ b_h
+    np.testing.assert_array_equal(np.isnan(c), np.isnan(want))
+    np.testing.assert_array_equal(np.isinf(c), np.isinf(want))
+
+
+def test_gemm_fp_rejects_bad_arguments(gpu):
+    from bee_code_interpreter_fs_amd.ops import _native
+
+    lib = _native.lib()
+    assert lib.bk_gemm_fp(2, 0, 0, 8, 8, 8, 4, 4, 4, 4, 4, 4, None) == 1  # bf16 is not this kernel's
+    assert lib.bk_gemm_fp(1, 0, 0, 8, 8, 8, 4, 4, 4, 3, 4, 4, None) == 1  # lda < K
+    assert lib.bk_gemm_fp(1, 1, 0, 8, 8, 8, 4, 4, 4, 3, 4, 4, None) == 1  # A^T: lda < M
+    assert lib.bk_gemm_fp(1, 0, 0, 8, 8, 8, 0, 4, 4, 4, 4, 4, None) == 1  # empty
+
+
+def test_unmodified_numpy_matmul_under_offload(gpu, monkeypatch):
+    """``np.random.rand(n, n) @ np.random.rand(n, n)`` with the offload on:
+    the product is the f64 MFMA GEMM, the values numpy's to f64 rounding."""
+    from bee_code_interpreter_fs_amd.ops import numpy_offload
+
+    monkeypatch.setattr(numpy_offload, "_GEN", [])
+    numpy_offload.patch_numpy_random(np.random, setter=lambda o, k, v: monkeypatch.setattr(o, k, v, raising=False))
+    a = np.random.rand(1024, 1024)
+    b = np.random.rand(1024, 1024)
+    c = a @ b
+    assert isinstance(c, numpy_offload.OffloadArray) and c.on_device and c.dtype == np.float64
+    g = np.random.default_rng(3).standard_normal((2048, 512))  # 2**20 elements: the offload threshold
+    d = np.dot(g.T, g)  # a Generator draw, a .T view read in place
+    assert isinstance(d, numpy_offload.OffloadArray) and d.on_device
+    a_h, b_h, g_h = np.asarray(a), np.asarray(b), np.asarray(g)
+    _check(np.asarray(c), a_h, b_h, "float64")
+    _check(np.asarray(d), g_h.T, g_h, "float64")

@@ -112,17 +112,71 @@ def test_unsupported_calls_fall_back_with_one_warning(drv):
         np.testing.assert_array_equal(np.cumsum(x), np.cumsum(h))
 
 
-def test_matmul_of_f64_arrays_is_not_rounded_to_bf16(drv, monkeypatch):
+def test_matmul_of_f64_arrays_runs_at_numpy_precision(drv, monkeypatch):
+    """f64 products go to the f64 MFMA GEMM (gemm_fp), never the bf16 one."""
     rng = np.random.default_rng(0)
     a_h, b_h = rng.standard_normal((64, 32)), rng.standard_normal((32, 16))
     a, b = ops.asarray(a_h), ops.asarray(b_h)
-    with pytest.warns(npinterop.HostFallbackWarning):
+    drv.launches.clear()
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # no host fallback
         c = np.matmul(a, b)
-    np.testing.assert_allclose(c, a_h @ b_h, rtol=1e-12)  # numpy's f64 product, exactly
+    assert isinstance(c, ops.DeviceArray) and c.dtype == "float64" and c.shape == (64, 16)
+    assert [k[:2] for k in drv.launches] == [("gemm_fp", 1)], drv.launches
+    np.testing.assert_allclose(c.numpy(), a_h @ b_h, rtol=1e-12)
     monkeypatch.setenv("BEE_NUMPY_OFFLOAD_MATMUL", "bf16")
     c2 = np.matmul(a, b)  # opted in: the bf16 MFMA GEMM
-    assert isinstance(c2, ops.DeviceArray) and "gemm" in "".join(kernels(drv))
+    assert isinstance(c2, ops.DeviceArray) and "gemm," in ",".join(kernels(drv)) + ","
     np.testing.assert_allclose(c2.numpy(), a_h @ b_h, atol=0.3)
+
+
+def test_matmul_dtypes_views_vectors_and_host_operands(drv):
+    rng = np.random.default_rng(1)
+    a_h = rng.standard_normal((48, 40))
+    a = ops.asarray(a_h)
+    # a .T view is read in place: one GEMM with the transposed-A flag, no transpose pass
+    drv.launches.clear()
+    g = np.dot(a.T, a)
+    assert kernels(drv) == ["gemm_fp"] and drv.launches[0][-2:] == (True, False), drv.launches
+    np.testing.assert_allclose(g.numpy(), a_h.T @ a_h, rtol=1e-12, atol=1e-12)
+    # 1-D operands: numpy's vector rules
+    v_h = rng.standard_normal(40)
+    r = a @ ops.asarray(v_h)
+    assert r.shape == (48,)
+    np.testing.assert_allclose(r.numpy(), a_h @ v_h, rtol=1e-12)
+    # a host ndarray operand is uploaded once; the result stays on the device
+    h = rng.standard_normal((40, 8))
+    drv.launches.clear()
+    r2 = np.matmul(a, h)
+    assert isinstance(r2, ops.DeviceArray) and kernels(drv) == ["gemm_fp"]
+    np.testing.assert_allclose(r2.numpy(), a_h @ h, rtol=1e-12)
+    # f32 stays f32; f32 with a host int64 operand promotes to f64, as numpy does
+    a32 = ops.asarray(a_h.astype(np.float32))
+    c32 = np.matmul(a32, ops.asarray(h.astype(np.float32)))
+    assert c32.dtype == "float32" and drv.launches[-1][1] == 0
+    np.testing.assert_allclose(c32.numpy(), a_h.astype(np.float32) @ h.astype(np.float32), rtol=1e-5, atol=1e-5)
+    ints = np.arange(40 * 3).reshape(40, 3)
+    c64 = np.matmul(a32, ints)
+    assert c64.dtype == "float64" and c64.shape == (48, 3)
+    np.testing.assert_allclose(c64.numpy(), a_h.astype(np.float32).astype(np.float64) @ ints, rtol=1e-12)
+    # batched (3-D) and mismatched shapes: numpy's answer / error, on the host
+    with pytest.warns(npinterop.HostFallbackWarning):
+        np.testing.assert_allclose(np.matmul(a, np.ones((2, 40, 3))), a_h @ np.ones((2, 40, 3)))
+    with pytest.raises(ValueError):
+        np.matmul(a, np.ones((39, 3)))
+
+
+def test_reshape_keywords_follow_numpy(drv):
+    """np.reshape(x, newshape=...) kept its shape out (a flat
+    array came back) and copy=True returned an aliasing view."""
+    x = ops.asarray(np.arange(12.0))
+    r = np.reshape(x, newshape=(3, 4))
+    assert r.shape == (3, 4)
+    assert np.reshape(x, (4, 3)).shape == (4, 3) and np.reshape(x, shape=(2, 6)).shape == (2, 6)
+    with pytest.warns(npinterop.HostFallbackWarning):
+        c = np.reshape(x, (3, 4), copy=True)  # numpy's copy, not a device view
+    c[0, 0] = 99.0
+    assert float(x.numpy()[0]) == 0.0
 
 
 def test_out_argument_writes_in_place(drv):
@@ -202,6 +256,21 @@ def test_operators_inplace_and_statistics(offload):
     assert x.astype(np.float32).dtype == np.float32
 
 
+def test_offloaded_matrices_multiply_on_the_device(offload):
+    """``np.random.rand(n, n) @ np.random.rand(n, n)``: both draws offloaded,
+    the product on the f64 GEMM, an OffloadArray back."""
+    a = np.random.rand(128, 64)
+    b = np.random.rand(64, 96)
+    c = a @ b
+    assert isinstance(c, OffloadArray) and c.on_device and c.shape == (128, 96) and c.dtype == np.float64
+    assert "gemm_fp" in kernels(offload)
+    d = np.dot(a.T, np.ones(128))  # a host vector operand: uploaded, the result stays on the device
+    assert isinstance(d, OffloadArray) and d.on_device and d.shape == (64,)
+    a_h = np.asarray(a)  # (the first host operation moves an offloaded array to the host for good)
+    np.testing.assert_allclose(np.asarray(c), a_h @ np.asarray(b), rtol=1e-12)
+    np.testing.assert_allclose(np.asarray(d), a_h.sum(axis=0), rtol=1e-12)
+
+
 def test_payload_without_offload_is_plain_numpy(drv):
     assert type(np.random.rand(N)) is np.ndarray
 
@@ -239,3 +308,36 @@ def test_numpy_offload_field_reaches_the_sandbox(tmp_path):
         assert r.status_code == 200 and r.json()["stdout"] == "True ndarray\n", r.text
     finally:
         h.stop()
+
+
+def test_views_share_residency_with_their_base(offload):
+    """a reshape / ravel / T view moved to the host alone
+    stopped aliasing its base.  Now the first host operation on any view
+    moves the base, and every view aliases the one host buffer."""
+    a = np.random.rand(64 * 64)
+    b = a.reshape(64, 64)
+    c = np.reshape(a, (32, 128))
+    t = b.T
+    assert all(isinstance(v, OffloadArray) and v.on_device for v in (b, c, t))
+    b[0, 1] = 5.0  # the base and every view move to the host together
+    assert not a.on_device and not c.on_device and not t.on_device
+    assert a[1] == 5.0 and c[0, 1] == 5.0 and t[1, 0] == 5.0
+    a[2] = 7.0
+    assert b[0, 2] == 7.0 and np.ravel(a)[2] == 7.0
+
+
+def test_default_rng_draws_are_offloaded(offload):
+    rng = np.random.default_rng(42)
+    assert isinstance(rng, np.random.Generator)
+    x = rng.random(N)
+    assert isinstance(x, OffloadArray) and x.on_device
+    y = rng.standard_normal((128, 64))
+    assert isinstance(y, OffloadArray) and y.shape == (128, 64)
+    assert abs(float(np.mean(y))) < 0.05
+    assert type(rng.random(10)) is np.ndarray  # small: numpy
+    assert rng.integers(0, 10, 5).shape == (5,)  # no kernel: numpy's own, same bit generator
+    same = float(np.sum(np.random.default_rng(42).random(N)))
+    assert same == float(np.sum(np.random.default_rng(42).random(N)))  # seeded: reproducible
+    assert np.random.default_rng(rng) is rng
+    f32 = rng.random(N, dtype=np.float32)
+    assert f32.dtype == np.float32
