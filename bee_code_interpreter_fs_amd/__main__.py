@@ -178,7 +178,8 @@ def _pin_replica(config: Config, backend, index: int, pid: int) -> None:
     from .scheduler.topology import slot_cpus
 
     slot = backend.slots[index % len(backend.slots)]
-    cpus = slot_cpus(slot.gpu, slots=[s.gpu for s in backend.slots], factor=config.cpu_quota_pin_factor)
+    cpus = slot_cpus(slot.gpu, slots=[s.gpu for s in backend.slots], factor=config.cpu_quota_pin_factor,
+                     quota=config.cpu_quota_override or None)
     if cpus:
         try:
             os.sched_setaffinity(pid, cpus)

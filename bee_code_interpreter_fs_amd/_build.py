@@ -52,9 +52,10 @@ def _targets() -> List[Target]:
     k = os.path.join(CSRC, "kernels")
     ex = os.path.join(CSRC, "executor")
     q = os.path.join(CSRC, "hbm_quota")
-    # broker_fuzz.cpp is the CPU fuzz harness's main(), not part of the daemon
+    # broker_fuzz.cpp / admission_test.cpp are CPU test harnesses' main()s,
+    # not part of the daemon
     ex_srcs = sorted(os.path.join(ex, f) for f in os.listdir(ex)
-                     if f.endswith(".cpp") and f != "broker_fuzz.cpp") if os.path.isdir(ex) else []
+                     if f.endswith(".cpp") and f not in ("broker_fuzz.cpp", "admission_test.cpp")) if os.path.isdir(ex) else []
     ex_hdrs = sorted(os.path.join(ex, f) for f in os.listdir(ex) if f.endswith(".hpp")) if os.path.isdir(ex) else []
     rb = os.path.join(CSRC, "rccl_bench")
     targets = [
@@ -133,6 +134,22 @@ def _targets() -> List[Target]:
                 link_flags=["-fsanitize=address,undefined", "-static-libasan"],
                 shared=False,
                 headers=[os.path.join(ex, "broker_core.hpp")],
+            )
+        )
+    if ex_srcs:
+        # the admission state machine alone, under ThreadSanitizer: what
+        # tests/test_admission_unit_cpu.py drives (no daemon, no service)
+        targets.append(
+            Target(
+                name="admission-test",
+                output=os.path.join(ROOT, "build", "sanitize", "bee-admission-test"),
+                sources=[os.path.join(ex, "admission.cpp"), os.path.join(ex, "admission_test.cpp")],
+                compiler=CXX,
+                compile_flags=["-O1", "-g", "-std=c++17", "-Wall", "-Wextra", "-pthread", "-fsanitize=thread",
+                               "-fno-omit-frame-pointer", "-include", os.path.join(CSRC, "sanitize", "tsan_compat.hpp")],
+                link_flags=["-fsanitize=thread", "-pthread"],
+                shared=False,
+                headers=[os.path.join(ex, "admission.hpp"), os.path.join(CSRC, "sanitize", "tsan_compat.hpp")],
             )
         )
     fm = os.path.join(CSRC, "fsmap")

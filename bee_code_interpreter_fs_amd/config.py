@@ -180,6 +180,9 @@ class Config:
     # 4 -> 1939, 8 -> 3416 RPS at 4.0 ms (the 1-slot run's 4.2); one slot:
     # 2x cut CPU 15-20% but not latency (profiles/archive/r3_cpu_quota_pinning_ab.log)
     cpu_quota_pin_factor: float = 8.0
+    # the CPU quota the pinning assumes (0 = the cgroup's cpu.max): tests and
+    # rehearsals on hosts without a quota
+    cpu_quota_override: float = 0.0
     # a gang whose rank failed: seconds the other ranks get to finish before
     # the whole gang is killed (they are usually stuck in a collective)
     gang_failure_grace_s: float = 10.0
@@ -196,6 +199,13 @@ class Config:
     # gang request takes it like a pooled sandbox instead of forking N ranks
     # and initialising HIP on the request path.  [] = every gang starts cold
     gang_warm_sizes: List[int] = field(default_factory=lambda: [2, 4, 8])
+    # what one idle warm gang rank holds on its GPU (HIP context, torch's
+    # CUDA state, loaded kernels) and in host memory: charged against the
+    # slot's HBM and host-memory admission for every warm rank placed on it
+    # (one per warm gang size: 3 x on an 8-GPU node), so 24 idle ranks per
+    # node cannot overcommit either
+    gang_warm_rank_hbm_bytes: int = 1 << 30
+    gang_warm_rank_memory_bytes: int = 1 << 30
     # processes + threads per sandbox tree (the executor's monitor, any
     # mode; plus RLIMIT_NPROC of the sandbox UID in UID mode)
     sandbox_max_processes: int = 1024

@@ -628,6 +628,10 @@ def worker_main(spawn: dict) -> None:
 
         ctypes.CDLL(None, use_errno=True).prctl(36, 1, 0, 0, 0)  # PR_SET_CHILD_SUBREAPER
         env = spawn.get("env") or {}
+        if env.get("BEE_CPU_AFFINITY"):  # a gang rank: its GPU's slot CPUs (boot_child does the same)
+            from ..scheduler.topology import parse_cpulist
+
+            os.sched_setaffinity(0, parse_cpulist(env["BEE_CPU_AFFINITY"]))
         os.environ.update({k: str(v) for k, v in env.items()})
         for k in spawn.get("unset") or ():  # zygote-environment entries this sandbox must not have
             os.environ.pop(k, None)

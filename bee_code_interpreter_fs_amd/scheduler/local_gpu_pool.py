@@ -47,7 +47,7 @@ from ..services.storage import Storage
 from .backend import CodeExecutor, ExecuteRequest, ExecutionResult
 from .executor_process import ExecutorProcess
 from .load_table import LoadTable, open_table
-from .topology import slot_cpus
+from .topology import format_cpulist, slot_cpus
 from .uds_http import UdsHttpError
 
 logger = logging.getLogger("local_gpu_pool")
@@ -278,8 +278,7 @@ class LocalGpuPoolBackend(CodeExecutor):
             light_target=c.light_workers_per_gpu_target,
             broker=c.broker_enabled,
             light_zygotes=c.light_zygotes_per_gpu,
-            cpus=slot_cpus(gpu, slots=list(self.gpu_ids), factor=c.cpu_quota_pin_factor)
-            if (c.numa_affinity or "auto").lower() != "off" else None,
+            cpus=self._slot_cpus(gpu) or None,
             extra_args=["--max-idle", str(c.worker_max_idle_s), "--min-target", str(c.min_workers_per_gpu_target),
                         "--min-zygotes", str(c.min_zygotes_per_gpu),
                         "--min-cpu-target", str(c.min_cpu_workers_per_gpu_target),
@@ -289,6 +288,12 @@ class LocalGpuPoolBackend(CodeExecutor):
                         "--gang-grace", str(c.gang_failure_grace_s),
                         "--fault-spawn-fail-rate", repr(float(c.fault_spawn_fail_rate or 0.0)),
                         "--gang-warm", ";".join(self._gang_keys_led_by(i)),
+                        # gang ranks run next to their own GPU, not the lead's
+                        "--gang-cpus", ";".join(f"{g}={format_cpulist(cs)}" for g, cs in
+                                                ((g, self._slot_cpus(g)) for g in self.gpu_ids) if cs),
+                        # idle warm gang ranks on this GPU, charged up front
+                        "--standing-hbm", str(self._warm_ranks_on(i) * c.gang_warm_rank_hbm_bytes if gpu is not None else 0),
+                        "--standing-mem", str(self._warm_ranks_on(i) * c.gang_warm_rank_memory_bytes),
                         "--gang-env", ",".join(f"{k}={v}" for k, v in sorted((c.gang_rccl_env or {}).items())
                                                if "," not in f"{k}={v}"),
                         # admission for every front-end replica of the node
@@ -303,6 +308,23 @@ class LocalGpuPoolBackend(CodeExecutor):
                         "--cgroup", c.sandbox_cgroup or "auto", "--cgroup-root", c.sandbox_cgroup_root or "",
                         *isolation_args(c, i, [self.storage.storage_path])],
         )
+
+    def _slot_cpus(self, gpu: Optional[int]) -> List[int]:
+        """The CPUs GPU ``gpu``'s slot is pinned to ([] = not pinned)."""
+        c = self.config
+        if gpu is None or (c.numa_affinity or "auto").lower() == "off":
+            return []
+        return slot_cpus(gpu, slots=list(self.gpu_ids), factor=c.cpu_quota_pin_factor,
+                         quota=c.cpu_quota_override or None)
+
+    def _warm_ranks_on(self, slot: int) -> int:
+        """Idle warm gang ranks placed on slot ``slot``'s GPU: one per warm
+        gang size whose aligned block covers it (rank r of a set holds the
+        block's r-th GPU)."""
+        if not self.gpu_ids:
+            return 0
+        sizes = {int(x) for x in (self.config.gang_warm_sizes or []) if 1 < int(x) <= len(self.gpu_ids)}
+        return sum(1 for n in sizes for block in self._aligned_blocks(n) if slot in block)
 
     def _aligned_blocks(self, n: int) -> List[List[int]]:
         """Slot-index blocks a gang of ``n`` is placed on first: aligned runs

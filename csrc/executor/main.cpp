@@ -59,6 +59,7 @@ void usage() {
           "                    [--fault-spawn-fail-rate R]\n"
           "                    [--hbm-watchdog-ms MS] [--hbm-slack BYTES] [--max-inflight N] [--hbm-capacity BYTES]\n"
           "                    [--admit-timeout S] [--mem-capacity BYTES] [--sandbox-memory BYTES] [--sandbox-tasks N] [--sandbox-cpus C]\n"
+          "                    [--standing-hbm BYTES] [--standing-mem BYTES] [--gang-cpus GPU=LIST;...]\n"
           "                    [--monitor-ms MS] [--deny-ports P1,P2,...]\n"
           "                    [--cgroup auto|require|off|fake] [--cgroup-root DIR]\n");
 }
@@ -178,6 +179,20 @@ int main(int argc, char** argv) {
     else if (a == "--mem-capacity") cfg.mem_capacity = atoll(val().c_str());
     else if (a == "--sandbox-network") cfg.sandbox_network = val();
     else if (a == "--admit-timeout") cfg.admit_timeout_s = atof(val().c_str());
+    else if (a == "--standing-hbm") cfg.standing_hbm = atoll(val().c_str());
+    else if (a == "--standing-mem") cfg.standing_mem = atoll(val().c_str());
+    else if (a == "--gang-cpus") {  // "0=0-15;1=16-31": each GPU's slot CPUs, for the gang ranks placed on it
+      const std::string spec = val();
+      size_t i = 0;
+      while (i < spec.size()) {
+        size_t j = spec.find(';', i);
+        if (j == std::string::npos) j = spec.size();
+        const std::string kv = spec.substr(i, j - i);
+        const size_t eq = kv.find('=');
+        if (eq != std::string::npos && eq > 0 && eq + 1 < kv.size()) cfg.gang_cpus[kv.substr(0, eq)] = kv.substr(eq + 1);
+        i = j + 1;
+      }
+    }
     else if (a == "--sandbox-memory") cfg.sandbox_mem_bytes = atoll(val().c_str());
     else if (a == "--sandbox-tasks") cfg.sandbox_tasks = atoll(val().c_str());
     else if (a == "--sandbox-cpus") cfg.sandbox_cpus = atof(val().c_str());

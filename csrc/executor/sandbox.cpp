@@ -14,6 +14,14 @@ SandboxPool::SandboxPool(PoolConfig cfg) : cfg_(std::move(cfg)) {
   // Unix socket paths are capped at 107 bytes: deep sandbox roots get their
   // control sockets in a short private directory instead
   if (cfg_.run_dir.size() > 72) cfg_.run_dir = "/tmp/bee-run-" + random_hex(6);
+  AdmissionLimits lim;
+  lim.max_inflight = cfg_.max_inflight;
+  lim.hbm_capacity = cfg_.hbm_capacity;
+  lim.mem_capacity = cfg_.mem_capacity;
+  lim.standing_hbm = cfg_.hbm_capacity > 0 ? cfg_.standing_hbm : 0;
+  lim.standing_mem = cfg_.mem_capacity > 0 ? cfg_.standing_mem : 0;
+  lim.timeout_s = cfg_.admit_timeout_s;
+  admission_.reset(new Admission(lim));
 }
 
 SandboxPool::~SandboxPool() { stop(); }
@@ -126,18 +134,11 @@ bool SandboxPool::start(std::string* err) {
   light_ok_ = broker_ != nullptr || cpu_light;
   wake_fd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   fcntl(worker_listen_fd_, F_SETFL, fcntl(worker_listen_fd_, F_GETFL) | O_NONBLOCK);
-  // the load table front-end replicas route by (LoadTable)
-  load_path_ = join_path(cfg_.run_dir, "load-" + std::to_string(getpid()));
+  // the load table front-end replicas route by (admission.hpp)
   {
-    const int lfd = open(load_path_.c_str(), O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC | O_NOFOLLOW, 0600);
-    if (lfd >= 0 && ftruncate(lfd, 4096) == 0) {
-      void* m = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, lfd, 0);
-      if (m != MAP_FAILED) load_ = static_cast<LoadTable*>(m);
-    }
-    if (lfd >= 0) close(lfd);
-    if (!load_) BEE_WARN("load table %s unavailable: %s", load_path_.c_str(), strerror(errno));
-    std::lock_guard<std::mutex> lk(mu_);
-    publish_load_locked();
+    std::string lerr;
+    if (!admission_->map_load_table(join_path(cfg_.run_dir, "load-" + std::to_string(getpid())), &lerr))
+      BEE_WARN("load table unavailable: %s", lerr.c_str());
   }
   acceptor_thread_ = std::thread([this] { worker_acceptor(); });
   cleanup_thread_ = std::thread([this] { cleanup_loop(); });
@@ -191,6 +192,7 @@ void SandboxPool::stop() {
   }
   unlink(worker_sock_path_.c_str());
   cv_.notify_all();
+  if (admission_) admission_->wake_all();
   cleanup_cv_.notify_all();
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -203,31 +205,8 @@ void SandboxPool::stop() {
   if (acceptor_thread_.joinable()) acceptor_thread_.join();
   if (cleanup_thread_.joinable()) cleanup_thread_.join();
   if (watchdog_thread_.joinable()) watchdog_thread_.join();
-  if (load_) {
-    munmap(load_, 4096);
-    load_ = nullptr;
-    unlink(load_path_.c_str());
-  }
+  if (admission_) admission_->unmap_load_table();
 }
 
-void SandboxPool::publish_load_locked() {
-  if (!load_) return;
-  LoadTable* t = load_;
-  __atomic_store_n(&t->seq, t->seq + 1, __ATOMIC_RELEASE);  // odd: being written
-  __atomic_thread_fence(__ATOMIC_SEQ_CST);
-  t->magic = kLoadMagic;
-  t->jobs = jobs_;
-  t->waiting = (int64_t)admit_queue_.size();
-  t->hbm_committed = hbm_committed_;
-  t->max_inflight = cfg_.max_inflight;
-  t->hbm_capacity = cfg_.hbm_capacity;
-  t->reserved = reserved_ && mono_ms() < reserved_until_ ? 1 : 0;
-  t->executions = admitted_;
-  t->pid = getpid();
-  t->max_jobs_seen = max_jobs_seen_;
-  t->max_hbm_seen = max_hbm_seen_;
-  __atomic_thread_fence(__ATOMIC_SEQ_CST);
-  __atomic_store_n(&t->seq, t->seq + 1, __ATOMIC_RELEASE);
-}
 
 }  // namespace bee

@@ -62,6 +62,8 @@ void SandboxPool::refill_gangs_locked() {
         e.set("BEE_DEVICE", std::to_string(r));
       }
       if (r > 0 && cfg_.jail) e.set("BEE_JAIL_SHARED", join_path(dirname_of(ws0), "tmp"));
+      const std::string cpus = rank_cpus(key, r);
+      if (!cpus.empty()) e.set("BEE_CPU_AFFINITY", cpus);
       auto w = spawn_worker(false, kDirect, key, e, ws0, rp0, uid0, true);
       w->gang_key = key;
       if (r == 0) {
@@ -73,6 +75,11 @@ void SandboxPool::refill_gangs_locked() {
     }
     gang_sets_[key] = std::move(set);
   }
+}
+
+std::string SandboxPool::rank_cpus(const std::string& gpus, int r) const {
+  auto it = cfg_.gang_cpus.find(nth_gpu(gpus, r));
+  return it == cfg_.gang_cpus.end() ? std::string() : it->second;
 }
 
 std::vector<std::shared_ptr<Worker>> SandboxPool::take_gang_locked(const std::string& key) {

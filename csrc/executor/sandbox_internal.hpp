@@ -107,6 +107,30 @@ inline const char* state_name(WorkerState s) {
   return "?";
 }
 
+// A request env entry read when torch's CUDA state / caching allocator
+// initialises (PYTORCH_HIP_ALLOC_CONF, PYTORCH_CUDA_ALLOC_CONF,
+// PYTORCH_NO_CUDA_MEMORY_CACHING, ...): a warm gang rank did that before the
+// request existed, so such a request must start its ranks cold or the
+// setting would be silently ignored
+inline bool init_time_env(const Json& env) {
+  if (!env.is_object()) return false;
+  for (auto& kv : env.as_object())
+    if (kv.first.rfind("PYTORCH_", 0) == 0) return true;
+  return false;
+}
+
+// the r-th id of a "g0,g1,..." GPU list ("" past its end)
+inline std::string nth_gpu(const std::string& gpus, int r) {
+  size_t i = 0;
+  for (int k = 0; k < r; ++k) {
+    i = gpus.find(',', i);
+    if (i == std::string::npos) return std::string();
+    ++i;
+  }
+  const size_t j = gpus.find(',', i);
+  return gpus.substr(i, j == std::string::npos ? std::string::npos : j - i);
+}
+
 // the request-independent environment of gang rank r of n (sandbox_gang.cpp)
 Json gang_rank_env(int r, int n, const std::vector<std::pair<std::string, std::string>>& gang_env);
 

@@ -86,21 +86,25 @@ Json SandboxPool::status() {
   }
   {
     Json adm = Json::object();
+    const AdmissionSnapshot a = admission_->snapshot();
     adm.set("max_inflight", (int64_t)cfg_.max_inflight);
     adm.set("hbm_capacity", cfg_.hbm_capacity);
-    adm.set("jobs", jobs_);
-    adm.set("waiting", (int64_t)admit_queue_.size());
-    adm.set("hbm_committed", hbm_committed_);
-    adm.set("max_jobs_seen", max_jobs_seen_);
-    adm.set("max_hbm_seen", max_hbm_seen_);
+    adm.set("jobs", a.jobs);
+    adm.set("waiting", a.waiting);
+    adm.set("hbm_committed", a.hbm_committed);
+    adm.set("max_jobs_seen", a.max_jobs_seen);
+    adm.set("max_hbm_seen", a.max_hbm_seen);
     adm.set("mem_capacity", cfg_.mem_capacity);
-    adm.set("mem_committed", mem_committed_);
-    adm.set("max_mem_seen", max_mem_seen_);
+    adm.set("mem_committed", a.mem_committed);
+    adm.set("max_mem_seen", a.max_mem_seen);
+    adm.set("standing_hbm", admission_->limits().standing_hbm);
+    adm.set("standing_mem", admission_->limits().standing_mem);
     adm.set("sandbox_mem_bytes", cfg_.sandbox_mem_bytes);
-    adm.set("admitted", admitted_);
-    adm.set("busy_429", (int64_t)m_admit_busy_.load());
-    adm.set("timeouts", (int64_t)m_admit_timeouts_.load());
-    adm.set("load_table", load_ ? load_path_ : std::string());
+    adm.set("admitted", a.admitted);
+    adm.set("reserved", a.reserved);
+    adm.set("busy_429", a.busy);
+    adm.set("timeouts", a.timeouts);
+    adm.set("load_table", admission_->load_mapped() ? admission_->load_path() : std::string());
     j.set("admission", adm);
     Json con = Json::object();
     con.set("memory_bytes", cfg_.sandbox_mem_bytes);
@@ -166,10 +170,11 @@ std::string SandboxPool::metrics_text() {
   line("bee_executor_memory_limit_kills_total", "counter", (double)m_mem_kills_.load());
   line("bee_executor_task_limit_kills_total", "counter", (double)m_task_kills_.load());
   line("bee_executor_cpu_throttles_total", "counter", (double)m_throttles_.load());
-  line("bee_executor_admission_busy_total", "counter", (double)m_admit_busy_.load());
-  line("bee_executor_admitted_jobs", "gauge", (double)jobs_);
-  line("bee_executor_admission_waiting", "gauge", (double)admit_queue_.size());
-  line("bee_executor_hbm_committed_bytes", "gauge", (double)hbm_committed_);
+  const AdmissionSnapshot adm = admission_->snapshot();
+  line("bee_executor_admission_busy_total", "counter", (double)adm.busy);
+  line("bee_executor_admitted_jobs", "gauge", (double)adm.jobs);
+  line("bee_executor_admission_waiting", "gauge", (double)adm.waiting);
+  line("bee_executor_hbm_committed_bytes", "gauge", (double)adm.hbm_committed);
   s += "# TYPE bee_executor_cpu_seconds_total counter\n";
   for (int i = 0; i < kCpuParts; ++i)
     s += std::string("bee_executor_cpu_seconds_total{gpus=\"") + cfg_.gpus + "\",part=\"" + kCpuPartNames[i] + "\"} " +

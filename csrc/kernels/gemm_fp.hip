@@ -43,17 +43,12 @@ namespace fp {
 constexpr int kBM = 128, kBN = 128, kThreads = 256;
 constexpr int kPitchMN = 128 + 16;  // LDS row of an [k][m|n] tile: 144 elements
 
+// K tile: 128 B per row by default (16 f64 / 32 f32); an [m|n][k] LDS row is
+// padded by 16 B so a fragment read (16 rows x 4 k) hits 64 distinct banks
 template <typename T>
-struct Cfg;
-// K tile = 128 B per row; an [m|n][k] LDS row is padded by 16 B so a
-// fragment read (16 rows x 4 k) hits 64 distinct banks
-template <>
-struct Cfg<double> {
-  static constexpr int BK = 16, kPitchK = 18;
-};
-template <>
-struct Cfg<float> {
-  static constexpr int BK = 32, kPitchK = 36;
+struct Cfg {
+  static constexpr int kDefaultBK = 128 / sizeof(T);
+  static constexpr int pitch_k(int bk) { return bk + 16 / (int)sizeof(T); }
 };
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -138,11 +133,11 @@ struct Tile {
 // b[TB ? n*ldb + k : k*ldb + n].  Workgroup tile 128 x BN (BN = 128, or 64
 // when 128^2 tiles would leave CUs with a single workgroup); 4 waves of
 // 64 x BN/2.
-template <typename T, bool TA, bool TB, bool VEC, int BN>
-__global__ __launch_bounds__(kThreads, 2) void gemm_fp_kernel(const T* __restrict__ a, const T* __restrict__ b,
+template <typename T, bool TA, bool TB, bool VEC, int BN, int BK, int OCC>
+__global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restrict__ a, const T* __restrict__ b,
                                                                T* __restrict__ c, int M, int N, int K, int64_t lda,
                                                                int64_t ldb, int64_t ldc) {
-  constexpr int BK = Cfg<T>::BK, PK = Cfg<T>::kPitchK;
+  constexpr int PK = Cfg<T>::pitch_k(BK);
   constexpr int kPitchN = BN + 16;  // a [k][n] row: f64 = 32, f32 = 16 dwords mod 64 banks
   constexpr int WN = BN / 2, NT = WN / 16;  // wave columns, 16-wide MFMA tiles per wave row
   // A tile: [m][k] (row-major A) or [k][m] (A^T view); B tile: [k][n] or [n][k]
@@ -262,23 +257,39 @@ inline bool narrow_tiles(int M, int N) {
   return t128 < 2 * kNumCU && N > 64;
 }
 
+// Tile shape and depth.  BK_GEMM_FP_BN (64 | 128) and BK_GEMM_FP_BK (a K
+// depth in elements) override the choice for A/B runs (tools/gemm_fp_bench.py).
 template <typename T, bool TA, bool TB>
 void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, bool vec,
             hipStream_t stream) {
-  const bool nar = getenv("BK_GEMM_FP_BN") ? atoi(getenv("BK_GEMM_FP_BN")) == 64 : narrow_tiles(M, N);
+  const char* ebn = getenv("BK_GEMM_FP_BN");
+  const char* ebk = getenv("BK_GEMM_FP_BK");
+  const bool nar = ebn ? atoi(ebn) == 64 : narrow_tiles(M, N);
+  // f32: a 64-byte K tile (16 deep) halves the LDS a workgroup holds, so a
+  // CU keeps three of them resident (its registers allow it) instead of two
+  const int bk_default = std::is_same<T, float>::value ? 16 : Cfg<T>::kDefaultBK;
+  const int bk = ebk ? atoi(ebk) : bk_default;
   const int bn = nar ? 64 : 128;
   const unsigned grid = (unsigned)(((M + kBM - 1) / kBM) * ((N + bn - 1) / bn));
-#define BK_FP_LAUNCH(V, W)                                                                                       \
-  gemm_fp_kernel<T, TA, TB, V, W><<<grid, kThreads, 0, stream>>>((const T*)A, (const T*)B, (T*)C, M, N, K, lda, \
-                                                                 ldb, ldc)
-  if (vec && nar)
-    BK_FP_LAUNCH(true, 64);
-  else if (vec)
-    BK_FP_LAUNCH(true, 128);
-  else if (nar)
-    BK_FP_LAUNCH(false, 64);
+#define BK_FP_LAUNCH(V, W, D, O)                                                                                     \
+  gemm_fp_kernel<T, TA, TB, V, W, D, O><<<grid, kThreads, 0, stream>>>((const T*)A, (const T*)B, (T*)C, M, N, K, lda, \
+                                                                       ldb, ldc)
+#define BK_FP_DEPTH(D, O)          \
+  do {                             \
+    if (vec && nar)                \
+      BK_FP_LAUNCH(true, 64, D, O);  \
+    else if (vec)                  \
+      BK_FP_LAUNCH(true, 128, D, O); \
+    else if (nar)                  \
+      BK_FP_LAUNCH(false, 64, D, O); \
+    else                           \
+      BK_FP_LAUNCH(false, 128, D, O); \
+  } while (0)
+  if (std::is_same<T, float>::value && bk == 16)
+    BK_FP_DEPTH(16 * sizeof(float) / sizeof(T), 3);
   else
-    BK_FP_LAUNCH(false, 128);
+    BK_FP_DEPTH(Cfg<T>::kDefaultBK, 2);
+#undef BK_FP_DEPTH
 #undef BK_FP_LAUNCH
 }
 

@@ -1,4 +1,4 @@
-// Force-included into the TSan build of bee-executor only.  GCC 11's TSan
+// Force-included into the TSan builds (bee-executor-tsan, bee-admission-test).  GCC 11's TSan
 // runtime does not intercept pthread_cond_clockwait, which libstdc++ uses for
 // condition_variable::wait_for on steady_clock; TSan then misses the mutex
 // release inside the wait and reports a double lock plus false races on

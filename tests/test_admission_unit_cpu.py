@@ -1,0 +1,36 @@
+"""The executor's admission state machine (csrc/executor/admission.cpp) on
+its own, under ThreadSanitizer: tickets served in arrival order, the
+in-flight / HBM / host-memory bounds, standing commitments of idle warm gang
+ranks, try-only answers, time-outs, gang reservations (drain, bypass, TTL),
+shutdown, a many-thread stress run and the load table -- no daemon and no
+service harness (VERDICT r4 "next" #8).  The daemon-level behaviour is in
+tests/test_admission_cpu.py."""
+
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "build", "sanitize", "bee-admission-test")
+CASES = ["fifo_order", "hbm_commitment", "mem_commitment", "standing_commitments", "timeout", "reservation",
+         "stopping", "stress", "load_table"]
+
+
+@pytest.fixture(scope="module")
+def admission_bin():
+    from bee_code_interpreter_fs_amd import _build
+
+    _build.build(["admission-test"], verbose=False)
+    assert os.path.exists(BIN)
+    return BIN
+
+
+def test_admission_state_machine(admission_bin, tmp_path):
+    p = subprocess.run([admission_bin, str(tmp_path)], capture_output=True, text=True, timeout=120,
+                       env={**os.environ, "TSAN_OPTIONS": "halt_on_error=1"})
+    out = p.stdout + p.stderr
+    assert "ThreadSanitizer" not in out, out[-4000:]
+    for case in CASES:
+        assert f"PASS {case}" in p.stdout, out[-4000:]
+    assert p.returncode == 0, out[-4000:]
