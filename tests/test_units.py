@@ -387,6 +387,11 @@ def test_sandbox_mode_routing(tmp_path):
     assert mode("exec('import pandas as pd')\nprint(pd)") == "light"
     assert mode("import beekern as bk\nmod = __import__('json')") == "light"
     assert mode("import torch\nimport importlib") == "direct"
+    # methods named like the builtins are no dynamic import:
+    # re.compile / obj.eval stay on the numpy-free sandboxes
+    assert mode("import re\nprint(re.compile('a+').match('aa'))") == "nano_cpu"
+    assert mode("import numpy as np\nclass M:\n    def eval(self): return 1\nM().eval()") == "min_cpu"
+    assert mode("code = compile('1 + 1', 'x', 'eval')") == "light"
 
 
 def test_philox_reference_known_answers():
