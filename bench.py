@@ -619,33 +619,64 @@ def run_loadgens(n_procs, targets, source, concurrency, warmup, steps, sync, mar
     return out
 
 
-GANG_SCRIPT = """
-import os, time, torch, torch.distributed as dist
+# The gang check's job (BASELINE config 5): an all-reduce over the gang's
+# ranks, its bus bandwidth per message size against the xGMI budget, the
+# small-message latency, and the RCCL environment the ranks actually run
+# with.  On GPUs: "nccl" (RCCL over xGMI); in the virtual-GPU CPU rehearsal:
+# "gloo" on CPU tensors (smaller messages), every other step the same.
+GANG_SCRIPT_TEMPLATE = """
+import json, os, time, torch, torch.distributed as dist
 t0 = time.perf_counter()
 rank = int(os.environ["RANK"]); world = int(os.environ["WORLD_SIZE"])
-torch.cuda.set_device(int(os.environ["LOCAL_RANK"]))
-dist.init_process_group("nccl")  # the gang's FileStore rendezvous (BEE_GANG_RDZV)
+backend = "{backend}"
+dev = "cuda" if backend == "nccl" else "cpu"
+if dev == "cuda":
+    torch.cuda.set_device(int(os.environ["LOCAL_RANK"]))
+def sync():
+    if dev == "cuda":
+        torch.cuda.synchronize()
+dist.init_process_group(backend)  # the gang's FileStore rendezvous (BEE_GANG_RDZV)
 t_init = time.perf_counter()
-x = torch.full((64 << 20,), float(rank + 1), device="cuda")  # 256 MB f32
-dist.all_reduce(x); torch.cuda.synchronize()
+x = torch.full(({big},), float(rank + 1), device=dev)  # the large message, f32
+dist.all_reduce(x); sync()
 want = world * (world + 1) / 2
 ok = bool((x[:4096] == want).all()) and bool((x[-4096:] == want).all())
-s = torch.ones((1024,), device="cuda")  # 4 KiB: latency
+s = torch.ones((1024,), device=dev)  # 4 KiB: latency
 for _ in range(5):
     dist.all_reduce(s)
-torch.cuda.synchronize(); t = time.perf_counter()
+sync(); t = time.perf_counter()
 for _ in range(50):
     dist.all_reduce(s)
-torch.cuda.synchronize(); small_us = (time.perf_counter() - t) / 50 * 1e6
-t = time.perf_counter(); iters = 10
-for _ in range(iters):
-    dist.all_reduce(x)
-torch.cuda.synchronize(); dt = (time.perf_counter() - t) / iters
-busbw = 2 * (world - 1) / world * x.numel() * 4 / dt / 1e9
+sync(); small_us = (time.perf_counter() - t) / 50 * 1e6
+sizes = []
+for numel in {sweep}:  # bus bandwidth per message size
+    m = x[:numel]
+    dist.all_reduce(m); sync()
+    iters = max(3, min(20, (64 << 20) // (numel * 4)))
+    t = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(m)
+    sync(); dt = (time.perf_counter() - t) / iters
+    sizes.append((numel * 4, 2 * (world - 1) / world * numel * 4 / dt / 1e9))
+busbw = sizes[-1][1]
 if rank == 0:
-    print(f"allreduce_ok={ok} busbw_GBps={busbw:.1f} small_us={small_us:.1f} init_ms={(t_init - t0) * 1e3:.0f}")
+    env = {{k: v for k, v in sorted(os.environ.items()) if k.startswith(("NCCL_", "RCCL_"))}}
+    ver = ".".join(map(str, torch.cuda.nccl.version())) if dev == "cuda" else None
+    print(f"allreduce_ok={{ok}} busbw_GBps={{busbw:.1f}} small_us={{small_us:.1f}} init_ms={{(t_init - t0) * 1e3:.0f}}")
+    print("gang_sizes=" + json.dumps([[b, round(g, 2)] for b, g in sizes]))
+    print("gang_env=" + json.dumps({{"backend": backend, "rccl_version": ver, "env": env}}))
 dist.destroy_process_group()
 """
+
+
+def gang_script(virtual: bool) -> str:
+    if virtual:  # CPU rehearsal: gloo, up to 16 MB
+        return GANG_SCRIPT_TEMPLATE.format(backend="gloo", big=4 << 20, sweep=[1 << 14, 1 << 18, 4 << 20])
+    # 64 KiB .. 256 MB: latency-bound, LL128 / simple protocol range, link-bound
+    return GANG_SCRIPT_TEMPLATE.format(backend="nccl", big=64 << 20, sweep=[1 << 14, 1 << 18, 1 << 22, 64 << 20])
+
+
+GANG_SCRIPT = gang_script(False)
 
 
 def _gang_warm_state(hport, n):
@@ -662,7 +693,7 @@ def _gang_warm_state(hport, n):
         return None, None, None
 
 
-def gang_allreduce_check(target, n, repeats=2, hport=None):
+def gang_allreduce_check(target, n, repeats=2, hport=None, virtual=False):
     """BASELINE config 5: an N-GPU torch.distributed (RCCL) job inside one
     gang sandbox, dispatched through the service like any other request --
     ``repeats`` back to back, each timed end to end (the ranks are spawned
@@ -686,8 +717,9 @@ def gang_allreduce_check(target, n, repeats=2, hport=None):
             # one run with more channels over the 7-link xGMI mesh set in the
             # script itself (RCCL reads the env at communicator init): the
             # node's own measurement of that knob, reported side by side
-            variants = [("default", GANG_SCRIPT)] * repeats + [
-                ("NCCL_MIN_NCHANNELS=112", "import os\nos.environ['NCCL_MIN_NCHANNELS'] = '112'\n" + GANG_SCRIPT)]
+            script0 = gang_script(virtual)
+            variants = [("default", script0)] * repeats + ([] if virtual else [
+                ("NCCL_MIN_NCHANNELS=112", "import os\nos.environ['NCCL_MIN_NCHANNELS'] = '112'\n" + script0)])
             for policy, script in variants:
                 left = end - time.monotonic()
                 if left < 30:
@@ -722,6 +754,13 @@ def gang_allreduce_check(target, n, repeats=2, hport=None):
                     kv = dict(p.split("=", 1) for p in line[0].split())
                     run.update(ok=kv.get("allreduce_ok") == "True", busbw_GBps=float(kv.get("busbw_GBps", "nan")),
                                small_allreduce_us=float(kv.get("small_us", "nan")), init_ms=float(kv.get("init_ms", "nan")))
+                    for l in r.stdout.splitlines():
+                        if l.startswith("gang_sizes="):
+                            run["busbw_by_size"] = [
+                                {"bytes": b, "busbw_GBps": g, "of_budget": round(g / out["budget_GBps"], 3)}
+                                for b, g in json.loads(l.split("=", 1)[1])]
+                        elif l.startswith("gang_env=") and "rccl_env" not in out:
+                            out["rccl_env"] = json.loads(l.split("=", 1)[1])
                 elif r.exit_code:
                     run["stderr_tail"] = r.stderr[-300:]
                 out["runs"].append(run)
@@ -736,6 +775,11 @@ def gang_allreduce_check(target, n, repeats=2, hport=None):
         out["busbw_GBps"] = max(r["busbw_GBps"] for r in ok)
         out["busbw_of_budget"] = round(out["busbw_GBps"] / out["budget_GBps"], 3)
         out["latency_ms"] = [r["latency_ms"] for r in out["runs"]]
+        best = max(ok, key=lambda r: r["busbw_GBps"])
+        if best.get("busbw_by_size"):
+            out["busbw_by_size"] = best["busbw_by_size"]  # the service policy's best run, per message size
+    out["transport"] = "gloo over loopback (virtual-GPU CPU rehearsal)" if virtual else "RCCL over xGMI"
+    out["budget_s"] = float(os.environ.get("BEE_BENCH_GANG_BUDGET_S", "240"))
     return out
 
 
@@ -976,7 +1020,7 @@ def main():
             # (a gang needs n distinct GPUs: RCCL refuses two ranks on one
             # device, so a folded rehearsal skips it)
             gang = (
-                gang_allreduce_check(target, n_gpus, hport=hport)
+                gang_allreduce_check(target, n_gpus, hport=hport, virtual=args.virtual_gpus)
                 if n_gpus > 1 and not args.no_gang_check and not args.cpu_only and len(set(ids)) >= n_gpus
                 else None
             )
@@ -1076,6 +1120,10 @@ def main():
                 bound["bound_by"] = "cpu" if out["value"] >= 0.85 * cap or cpu_busy >= 0.9 * quota else \
                     "latency/gpu at this concurrency"
             out["node_bound"] = bound
+            # next to the measured value: the rate this node's CPU quota allows
+            # at the measured CPU per Execute -- a flat 1 -> N curve explains
+            # itself when value sits at it
+            out["cpu_bound_rps"] = bound.get("cpu_bound_rps")
             out["pss_mb"] = pss_by_role(svc_pid)
             if slots0 and slots1 and len(slots0) == len(slots1):
                 per_slot = [b - a for a, b in zip(slots0, slots1)]

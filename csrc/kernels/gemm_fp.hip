@@ -22,8 +22,8 @@
 //  * K tile of 128 bytes per row (16 f64 / 32 f32): 16 KiB per operand, two
 //    LDS stages per operand = 72 KiB, so two workgroups share a CU and one's
 //    barrier hides behind the other's MFMAs;
-//  * global -> registers -> LDS, one barrier per K tile: the next tile's
-//    16-B loads are in flight during the current tile's MFMAs;
+//  * global -> registers -> LDS, two K tiles ahead, one barrier per K tile:
+//    a tile's 16-B loads are in flight during a whole tile of MFMAs;
 //  * LDS holds each operand tile in its global orientation (rows copied as
 //    16-B chunks), padded so the fragment reads are bank-conflict free in
 //    either orientation -- so A^T / B^T views (numpy's a.T, e.g. np.dot(a.T,
@@ -193,14 +193,30 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
     }
   };
 
+  // Pipeline (two LDS stages, one register stage, loads two K tiles ahead):
+  // iteration kt first stores tile kt+1 -- loaded during iteration kt-1 --
+  // into the other LDS stage (last read in iteration kt-1, before the
+  // barrier that ended it), then issues tile kt+2's global loads into the
+  // freed registers, then runs tile kt's MFMAs.  The loads get a whole
+  // iteration of MFMAs to land before the next iteration stores them, and
+  // the one barrier per tile orders both the stage's reads and its writes.
+  // (The one-ahead loop this replaced waited for its loads right before the
+  // barrier: rocprofv3 SQ_WAIT_ANY 18% of f32 wave cycles against
+  // torch.matmul's 3%, profiles/r5_gemm_fp_pmc.md.)
   const int nk = (K + BK - 1) / BK;
   load(0);
   ta.store(lds_a[0]);
   tb.store(lds_b[0]);
+  if (nk > 1) load(BK);
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      ta.store(lds_a[cur ^ 1]);
+      tb.store(lds_b[cur ^ 1]);
+      if (kt + 2 < nk) load((kt + 2) * BK);
+    }
     const T* As = lds_a[cur];
     const T* Bs = lds_b[cur];
 #pragma unroll
@@ -220,14 +236,6 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
-      // the next tile's loads go out behind the first k-step's MFMAs, so
-      // this tile's first fragment reads are not queued behind them
-      if (kk == 0 && kt + 1 < nk) load((kt + 1) * BK);
-    }
-    if (kt + 1 < nk) {
-      // the other stage was last read before the previous barrier
-      ta.store(lds_a[cur ^ 1]);
-      tb.store(lds_b[cur ^ 1]);
     }
     __syncthreads();
   }
@@ -285,10 +293,14 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
     else                           \
       BK_FP_LAUNCH(false, 128, D, O); \
   } while (0)
-  if (std::is_same<T, float>::value && bk == 16)
-    BK_FP_DEPTH(16 * sizeof(float) / sizeof(T), 3);
-  else
-    BK_FP_DEPTH(Cfg<T>::kDefaultBK, 2);
+  if constexpr (std::is_same<T, float>::value) {
+    if (bk == 16)
+      BK_FP_DEPTH(16, 3);
+    else
+      BK_FP_DEPTH(32, 2);
+  } else {
+    BK_FP_DEPTH(16, 2);
+  }
 #undef BK_FP_DEPTH
 #undef BK_FP_LAUNCH
 }

@@ -165,3 +165,49 @@ def test_cpu_throttle_reads_both_cgroup_versions(tmp_path):
     d = bench.throttle_delta(a, {"periods": 50, "throttled": 5, "throttled_ms": 40.0})
     assert d == {"periods": 10, "throttled_periods": 2, "throttled_ms": 15.0}
     assert bench.throttle_delta({}, a) is None
+
+
+# the keys a multi-GPU bench line carries (VERDICT r4 "next" #5): the driver's
+# first run on the 8-GPU node must explain itself without another run
+N_GPU_KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "p50_latency_ms", "completed", "errors", "per_gpu_rps",
+              "cpu_bound_rps", "node_bound", "executors", "slot_balance", "gang_allreduce"}
+GANG_KEYS = {"gpus", "budget_GBps", "runs", "ok", "busbw_GBps", "busbw_of_budget", "busbw_by_size", "rccl_env",
+             "transport", "budget_s"}
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_multi_gpu_bench_path_end_to_end_with_the_gang_check(n):
+    """The whole N-GPU bench path on N virtual GPU slots: load over every
+    slot, then the gang check -- an N-rank all-reduce sandbox through the
+    service (gloo on CPU where the node runs RCCL) with its per-size bus
+    bandwidth against the budget, the collective environment the ranks saw,
+    and its time budget -- and the JSON schema of an N > 1 line."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    env["BEE_BENCH_GANG_BUDGET_S"] = "200"
+    p = subprocess.run(
+        [sys.executable, "bench.py", "--gpus", str(n), "--virtual-gpus", "--workload", "hello", "--steps", "3",
+         "--warmup", "1", "--concurrency", "2", "--idle-probe", "0"],
+        cwd=ROOT, env=env, capture_output=True, text=True, timeout=900,
+    )
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([line for line in p.stdout.splitlines() if line.startswith("{")][-1])
+    missing = N_GPU_KEYS - set(out)
+    assert not missing, (missing, sorted(out))
+    assert out["n_gpus"] == n and out["errors"] == 0 and out["completed"] == n * 2 * 3, out
+    assert out["cpu_bound_rps"] == out["node_bound"].get("cpu_bound_rps")
+    g = out["gang_allreduce"]
+    assert not (GANG_KEYS - set(g)), (GANG_KEYS - set(g), g)
+    assert g["ok"] and g["gpus"] == n and g["transport"].startswith("gloo"), g
+    assert [s["bytes"] for s in g["busbw_by_size"]] == [1 << 16, 1 << 20, 16 << 20], g["busbw_by_size"]
+    assert all(s["busbw_GBps"] > 0 and s["of_budget"] == round(s["busbw_GBps"] / g["budget_GBps"], 3)
+               for s in g["busbw_by_size"])
+    assert g["rccl_env"]["backend"] == "gloo" and g["rccl_env"]["env"].get("NCCL_IB_DISABLE") == "1", g["rccl_env"]
+    assert g["budget_s"] == 200.0
+    assert all(r["rank_start"] in ("warm", "cold") for r in g["runs"]), g["runs"]
+    assert len(out["slot_balance"]["executions"]) == n

@@ -1,0 +1,60 @@
+"""Table of the f64 / f32 GEMM counter passes (tools/gemm_fp_pmc.sh):
+per-wave cycles by state, MFMA busy share, instruction mix -- beekern's
+kernel against torch.matmul's on the same operands.
+
+    python tools/gemm_fp_pmc.py gpurun_out DTYPE SIZE
+"""
+
+import glob
+import os
+import sqlite3
+import sys
+
+
+def load(d):
+    dbs = sorted(glob.glob(os.path.join(d, "**", "*results.db"), recursive=True))
+    out, dur = {}, None
+    for db in dbs:
+        con = sqlite3.connect(db)
+        cur = con.cursor()
+        rows = list(cur.execute("select kernel_name, counter_name, avg(value) from counters_collection "
+                                "group by kernel_name, counter_name"))
+        # the GEMM: the kernel with the most wave cycles (torch's fills are tiny)
+        by_k = {}
+        for k, c, v in rows:
+            by_k.setdefault(k, {})[c] = v
+        if not by_k:
+            continue
+        k = max(by_k, key=lambda n: by_k[n].get("SQ_WAVE_CYCLES", by_k[n].get("GRBM_GUI_ACTIVE", 0)))
+        out.update(by_k[k])
+        durs = {n: x for n, x in cur.execute("select name, avg(end - start) from kernels group by name")}
+        dur = durs.get(k, dur)
+        out["_kernel"] = k
+    return out, dur
+
+
+def main():
+    root, dt, n = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    print(f"| impl | kernel | us | GHz | wave cyc | busy | wait_any | wait_inst | wait_lds | MFMA busy | VALU insts/wave | LDS insts/wave |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
+    for impl in ("bk", "torch"):
+        v, dur = {}, None
+        for p in (1, 2):
+            a, d = load(os.path.join(root, f"pmc_{dt}_{n}_{impl}_{p}"))
+            v.update(a)
+            dur = dur or d
+        if not v or not dur:
+            print(f"| {impl} | (no data) |")
+            continue
+        waves = v.get("SQ_WAVES", 1)
+        q = lambda c: v.get(c, float("nan")) * 4 / waves  # noqa: E731  (quad-cycles -> cycles per wave)
+        clk = v["GRBM_GUI_ACTIVE"] / 8
+        busy = v.get("SQ_VALU_MFMA_BUSY_CYCLES", float("nan")) / (clk * 256 * 4)
+        print(f"| {impl} | {v['_kernel'][:48]} | {dur / 1e3:.1f} | {clk / dur:.2f} | {q('SQ_WAVE_CYCLES'):.0f} | "
+              f"{q('SQ_BUSY_CYCLES'):.0f} | {q('SQ_WAIT_ANY'):.0f} | {q('SQ_WAIT_INST_ANY'):.0f} | "
+              f"{q('SQ_WAIT_INST_LDS'):.0f} | {busy:.3f} | {v.get('SQ_INSTS_VALU', float('nan')) / waves:.0f} | "
+              f"{v.get('SQ_INSTS_LDS', float('nan')) / waves:.0f} |")
+
+
+if __name__ == "__main__":
+    main()
