@@ -133,11 +133,14 @@ struct Tile {
 // b[TB ? n*ldb + k : k*ldb + n].  Workgroup tile 128 x BN (BN = 128, or 64
 // when 128^2 tiles would leave CUs with a single workgroup); 4 waves of
 // 64 x BN/2.
-template <typename T, bool TA, bool TB, bool VEC, int BN, int BK, int OCC>
+template <typename T, bool TA, bool TB, bool VEC, int BN, int BK, int OCC, bool VF>
 __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restrict__ a, const T* __restrict__ b,
                                                                T* __restrict__ c, int M, int N, int K, int64_t lda,
                                                                int64_t ldb, int64_t ldc) {
   constexpr int PK = Cfg<T>::pitch_k(BK);
+  // vector fragment reads with a permuted k order (f32, BK % 16 == 0; f64's
+  // registers are too tight for the 2x fragment set); opt-in, BK_GEMM_FP_VEC=1
+  constexpr bool kVecFrag = std::is_same<T, float>::value && BK % 16 == 0 && VF;
   constexpr int kPitchN = BN + 16;  // a [k][n] row: f64 = 32, f32 = 16 dwords mod 64 banks
   constexpr int WN = BN / 2, NT = WN / 16;  // wave columns, 16-wide MFMA tiles per wave row
   // A tile: [m][k] (row-major A) or [k][m] (A^T view); B tile: [k][n] or [n][k]
@@ -219,6 +222,43 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
     }
     const T* As = lds_a[cur];
     const T* Bs = lds_b[cur];
+    if constexpr (kVecFrag) {
+      // f32: 16-B fragment reads.  The MFMA sums over k, so which k a lane
+      // contributes at which step is free as long as A and B agree: lane
+      // group g supplies k = kc + 4g + e at step e (of 4), so a lane's four
+      // A values for four steps are one ds_read_b128 of its [m][k] row (and
+      // B's too from an [n][k] view) instead of four ds_read_b32
+#pragma unroll
+      for (int kc = 0; kc < BK; kc += 16) {
+        f32x4 va[4], vb[NT];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = wm + i * 16 + fr;
+          if constexpr (!TA) {
+            va[i] = *reinterpret_cast<const f32x4*>(&As[m * PK + kc + 4 * fk]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) va[i][e] = As[(kc + 4 * fk + e) * kPitchMN + m];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int n = wn + j * 16 + fr;
+          if constexpr (TB) {
+            vb[j] = *reinterpret_cast<const f32x4*>(&Bs[n * PK + kc + 4 * fk]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) vb[j][e] = Bs[(kc + 4 * fk + e) * kPitchN + n];
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) acc[i][j] = mfma((T)va[i][e], (T)vb[j][e], acc[i][j]);
+      }
+    } else {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       T fa[4], fb[NT];
@@ -236,6 +276,7 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
+    }
     }
     __syncthreads();
   }
@@ -279,9 +320,19 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   const int bk = ebk ? atoi(ebk) : bk_default;
   const int bn = nar ? 64 : 128;
   const unsigned grid = (unsigned)(((M + kBM - 1) / kBM) * ((N + bn - 1) / bn));
-#define BK_FP_LAUNCH(V, W, D, O)                                                                                     \
-  gemm_fp_kernel<T, TA, TB, V, W, D, O><<<grid, kThreads, 0, stream>>>((const T*)A, (const T*)B, (T*)C, M, N, K, lda, \
-                                                                       ldb, ldc)
+  // vector fragment reads (BK_GEMM_FP_VEC=1): measured no faster on MI355X
+  // (4096^3 f32 126.7 vs 132.1 TFLOP/s, 8192^3 134.4 vs 135.0; their 5 more
+  // VGPRs cost a wave per SIMD), so the plain reads are the default
+  const bool vf = getenv("BK_GEMM_FP_VEC") && atoi(getenv("BK_GEMM_FP_VEC")) != 0;
+#define BK_FP_LAUNCH(V, W, D, O)                                                                              \
+  do {                                                                                                        \
+    if (vf && std::is_same<T, float>::value)                                                                  \
+      gemm_fp_kernel<T, TA, TB, V, W, D, O, std::is_same<T, float>::value><<<grid, kThreads, 0, stream>>>(     \
+          (const T*)A, (const T*)B, (T*)C, M, N, K, lda, ldb, ldc);                                             \
+    else                                                                                                      \
+      gemm_fp_kernel<T, TA, TB, V, W, D, O, false><<<grid, kThreads, 0, stream>>>((const T*)A, (const T*)B,     \
+                                                                                 (T*)C, M, N, K, lda, ldb, ldc); \
+  } while (0)
 #define BK_FP_DEPTH(D, O)          \
   do {                             \
     if (vec && nar)                \
