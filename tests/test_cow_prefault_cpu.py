@@ -1,0 +1,93 @@
+"""The zygote's copy-on-write prefault (csrc/zygote/zygote_loop.cpp,
+"copy-on-write prefault"), end to end on CPU.
+
+A sandbox writes ~600-700 of its zygote's pages, nearly the same ones every
+time; the zygote learns them from one "learner" sandbox (its pagemap at the
+end of the run) and every later sandbox copies them with
+MADV_POPULATE_WRITE right after fork, while it waits in the pool, instead of
+taking one fault apiece on its request path.  Checked here through the
+sandboxes' own debug stamps (BEE_DEBUG_NEW_MODULES=1):
+
+* learners report a non-trivial page set, and re-learning happens every
+  BEE_COW_RELEARN forks;
+* sandboxes forked after a set arrived prefault it (and take fewer faults
+  once the request is in);
+* outputs are unchanged -- the prefault is invisible to the program.
+"""
+
+import json
+import os
+import textwrap
+
+import pytest
+
+from .harness import ServiceHarness, ensure_native_executor
+
+PAYLOAD = textwrap.dedent(
+    """
+    import numpy as np
+    x = np.arange(1000, dtype=np.float64)
+    print("sum", float((x * x).sum()))
+    """
+)
+
+
+def _stamps(stderr: str) -> dict:
+    for line in stderr.splitlines():
+        if line.startswith("STAMPS "):
+            return json.loads(line[len("STAMPS "):])
+    return {}
+
+
+@pytest.fixture(scope="module")
+def service(tmp_path_factory):
+    ensure_native_executor()
+    saved = {k: os.environ.get(k) for k in ("BEE_DEBUG_NEW_MODULES", "BEE_COW_RELEARN", "BEE_COW_PREFAULT")}
+    os.environ.update({"BEE_DEBUG_NEW_MODULES": "1", "BEE_COW_RELEARN": "12", "BEE_COW_PREFAULT": "1"})
+    h = ServiceHarness(str(tmp_path_factory.mktemp("cow")), gpu_ids=[0], broker_enabled=False, worker_warm_gpu=False,
+                       workers_per_gpu_target=0, min_workers_per_gpu_target=4, light_workers_per_gpu_target=1,
+                       default_timeout=60.0)
+    try:
+        h.start()
+        yield h
+    finally:
+        h.stop()
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_learned_pages_are_prefaulted(service):
+    backend = service.ctx.code_executor
+    rows = []
+    for _ in range(36):
+        r = service.call(backend.execute(source_code=PAYLOAD), timeout=120)
+        assert r.exit_code == 0, r.stderr
+        assert r.stdout == "sum 332833500.0\n", r.stdout
+        st = _stamps(r.stderr)
+        st["w_minflt"] = r.timings_ms.get("w_minflt", 0)
+        rows.append(st)
+    learners = [s for s in rows if "cow_learned_pages" in s]
+    pre = [s for s in rows if s.get("cow_prefault_pages", 0) > 0]
+    plain = [s for s in rows if "cow_learned_pages" not in s and s.get("cow_prefault_pages", 0) == 0]
+    # a set per zygote, learned more than once over 36 forks at BEE_COW_RELEARN=12
+    assert len(learners) >= 2, [sorted(s) for s in rows[:3]]
+    assert all(s["cow_pagemap_open"] for s in learners), learners
+    assert all(s["cow_learned_pages"] >= 100 and s["cow_learned_runs"] >= 10 for s in learners), learners
+    # most sandboxes ran on a learned set
+    assert len(pre) >= len(rows) // 2, (len(pre), len(rows))
+    assert all(s["cow_prefault_pages"] <= 16384 for s in pre)
+    # the request path of a prefaulted sandbox faults less than a plain one's
+    if plain:
+        req = lambda s: s["w_minflt"] - s["minflt_pool"]  # noqa: E731
+        assert min(req(s) for s in pre) < min(req(s) for s in plain), ([req(s) for s in pre], [req(s) for s in plain])
+
+
+def test_module_state_outside_a_zygote():
+    from bee_code_interpreter_fs_amd.runtime import _zygote_loop
+
+    st = _zygote_loop.cow_stats()
+    assert st["learner"] is False and st["prefault_pages"] == 0 and st["hot_runs"] == 0
+    assert _zygote_loop.cow_report() is None  # not a learner: a no-op

@@ -19,17 +19,26 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=5)
+    ap.add_argument("--payload", default=os.path.join(ROOT, "examples", "benchmark_numpy_gpu.py"))
+    ap.add_argument("--cpu", action="store_true", help="no kernel broker (a CPU payload on a host without a GPU)")
+    ap.add_argument("--env", action="append", default=[], help="NAME=VALUE for the service (repeatable)")
     args = ap.parse_args()
+    for kv in args.env:
+        k, _, v = kv.partition("=")
+        os.environ[k] = v
     os.environ["BEE_DEBUG_NEW_MODULES"] = "1"
     os.environ["BEE_DEBUG_BOOT"] = "1"  # the zygote's C bootstrap, per step (lands in the executor log)
     os.environ["BEE_DEBUG_ZYGOTE_MEM"] = "1"  # each zygote's memory rollup (executor log)
     from tests.harness import ServiceHarness, ensure_native_executor
 
     ensure_native_executor()
-    src = open(os.path.join(ROOT, "examples", "benchmark_numpy_gpu.py")).read()
+    src = open(args.payload).read()
     tmp = tempfile.mkdtemp(prefix="bee-dbg-")
-    h = ServiceHarness(tmp, gpu_ids=[0], workers_per_gpu_target=1,
-                       min_workers_per_gpu_target=4, light_workers_per_gpu_target=1, default_timeout=120.0)
+    kw = dict(workers_per_gpu_target=1, min_workers_per_gpu_target=4, light_workers_per_gpu_target=1,
+              default_timeout=120.0)
+    if args.cpu:
+        kw.update(broker_enabled=False, worker_warm_gpu=False, workers_per_gpu_target=0)
+    h = ServiceHarness(tmp, gpu_ids=[0], **kw)
     h.start()
     try:
         for i in range(args.n):
