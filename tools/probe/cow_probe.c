@@ -2,7 +2,8 @@
 // 4 KB pages vs transparent huge pages, and how the pages a child writes are
 // spread over 2 MB regions (each first write into a shared huge page splits
 // its PMD in the child).  Prints one JSON line per case.
-//   cc -O2 -o /tmp/cow_probe tools/probe/cow_probe.c && /tmp/cow_probe
+//   cc -O2 -o /tmp/cow_probe tools/probe/cow_probe.c && /tmp/cow_probe [MB]
+//   env: COW_POPULATE=1 (MADV_POPULATE_WRITE first), COW_SETSID=1 (child setsid)
 #define _GNU_SOURCE
 #include <stdio.h>
 #include <stdlib.h>
@@ -27,7 +28,7 @@ static double now_ms(void) {
 }
 
 int main(int argc, char** argv) {
-  const size_t mb = argc > 1 ? atoi(argv[1]) : 64;
+  const size_t mb = argc > 1 && atoi(argv[1]) >= 4 ? atoi(argv[1]) : 64;
   const size_t size = mb << 20, huge = 2 << 20;
   const int reps = 20;
   for (int thp = 0; thp <= 1; ++thp) {
@@ -41,6 +42,7 @@ int main(int argc, char** argv) {
       memset(base, 1, size);
       if (thp) madvise(base, size, MADV_COLLAPSE);
       const int regions = (int)(size / huge);
+      const int r32 = regions < 32 ? regions : 32;  // (>= 1 MB: 512 pages fit in 2 regions)
       double fork_ms = 0, child_ms = 0, total_ms = 0, wall = 0;
       long flt = 0;
       for (int r = 0; r < reps; ++r) {
@@ -61,12 +63,15 @@ int main(int argc, char** argv) {
           for (int i = 0; i < 512; ++i) {
             size_t off;
             if (spread == 0) off = (size_t)i * 4096;
-            else if (spread == 1) off = (size_t)(i % 32) * huge + (size_t)(i / 32) * 4096;
+            else if (spread == 1) off = (size_t)(i % r32) * huge + (size_t)(i / r32) * 4096;
             else off = (size_t)(i % regions) * huge + (size_t)(i / regions) * 4096;
             base[off] = 2;
             ++n;
           }
           getrusage(RUSAGE_SELF, &c1);
+          // COW_SETSID=1: a session (and scheduler autogroup) of its own, as a
+          // sandbox leader has -- its creation and teardown land in exit_ms
+          if (getenv("COW_SETSID")) setsid();
           double v[2] = {cpu_ms(&c1) - cpu_ms(&c0), (double)(c1.ru_minflt - c0.ru_minflt)};
           write(pfd[1], v, sizeof v);
           _exit(0);
