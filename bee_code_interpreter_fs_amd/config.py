@@ -175,7 +175,7 @@ class Config:
     # the quota's worth of CPUs, split between the GPU slots (0 = NUMA only).
     # 8: each slot's daemon, zygotes and sandboxes keep to their own CPUs.
     # Measured on MI355X with 8 slots folded onto one GPU and a 16-CPU quota
-    # (bench.py --gpus 8 --fold, profiles/r4_fold_rehearsal.md): 0 -> 2402 RPS
+    # (bench.py --gpus 8 --fold, profiles/archive/r4_fold_rehearsal.md): 0 -> 2402 RPS
     # at 6.3 ms CPU per Execute, 2 -> 972 (4 CPUs a slot starve its zygotes),
     # 4 -> 1939, 8 -> 3416 RPS at 4.0 ms (the 1-slot run's 4.2); one slot:
     # 2x cut CPU 15-20% but not latency (profiles/archive/r3_cpu_quota_pinning_ab.log)

@@ -137,7 +137,7 @@ def slot_cpus(gpu: Optional[int], sysfs: str = "/sys", allowed: Optional[Set[int
     until its end (cpu.stat nr_throttled).  On MI355X, pinned to 32 CPUs:
     4.8-5.2 vs 5.8-7.2 ms of CPU per Execute, throughput within the boxes'
     noise on driver-length runs and lower on 600-step runs
-    (profiles/r3_cpu_quota_pinning_ab.log), so the service's default factor
+    (profiles/archive/r3_cpu_quota_pinning_ab.log), so the service's default factor
     is 0 (config.cpu_quota_pin_factor).  [] = no pinning."""
     if gpu is None:
         return []

@@ -291,7 +291,7 @@ class HipDevice final : public broker::Device {
   // the command processor dispatches them ahead of other sessions' queued
   // GEMMs and large passes (under 8 concurrent sandboxes a 6 us row sum
   // averaged 37 us and a 2.4 us reduction 19 us behind them,
-  // profiles/r3_final_served_kernels.csv).  One session's ops stay in issue
+  // profiles/archive/r3_final_served_kernels.csv).  One session's ops stay in issue
   // order: moving to the other stream records an event on the one it leaves
   // and makes the new one wait for it (GPU-side), and waits / deferred frees
   // follow the latest stream (which by this chain follows everything before).
@@ -412,7 +412,7 @@ class HipDevice final : public broker::Device {
   bool spin_wait_ = getenv("BEE_BROKER_WAIT") && !strcmp(getenv("BEE_BROKER_WAIT"), "spin");
   // BEE_BROKER_PRIO=1: short ops on a high-priority stream (pick()).  Off by
   // default: measured on MI355X (300 served headline Executes, 8 concurrent,
-  // profiles/r4_served_prio_ab.md) the high-priority queue let reductions
+  // profiles/archive/r4_served_prio_ab.md) the high-priority queue let reductions
   // start beside other sessions' GEMMs instead of after them, where they ran
   // slower and slowed the GEMMs: bk.reduce 181 vs 126 us and bk.rand_reduce
   // 525 vs 423 us per op, rowsum 39 vs 32 us per kernel, 2763-2835 vs

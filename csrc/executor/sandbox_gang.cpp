@@ -104,7 +104,7 @@ int SandboxPool::target_of(int kind) const {
   // kind (handle(): mode "nano_cpu" -> kNano), so the base pool is sized for
   // both: a CPU-only node's stdlib scripts otherwise queue on the few warm
   // sandboxes of the GPU-script pool (hello on a CPU-only executor: p50
-  // acquire 1.2 ms, 2755 vs 4531 RPS GPU-pinned, profiles/r4_bench_suite.jsonl)
+  // acquire 1.2 ms, 2755 vs 4531 RPS GPU-pinned, profiles/archive/r4_bench_suite.jsonl)
   if (kind == kLight) return light_ok_ ? cfg_.light_target : 0;
   if (kind == kMin)
     return light_ok_ && min_ok_ ? (!broker_ ? std::max(cfg_.min_target, cfg_.min_cpu_target) : cfg_.min_target) : 0;

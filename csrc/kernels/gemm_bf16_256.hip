@@ -19,7 +19,7 @@ constexpr int kShipped = g256::kOptRound1;
 // kernels.  Interleaved A/B on one MI355X (profiles/r4_gemm_pmc.md,
 // tools/gemm_lab.py): 4096^3 98.9 -> 94.5 us (hipBLASLt 93.6), 8192^3
 // 739 -> 705 us (hipBLASLt 671).  Before: kSpacedMem (M G M M r M groups,
-// profiles/r3_gemm_lab_spaced.log).
+// profiles/archive/r3_gemm_lab_spaced.log).
 constexpr long long kShippedW4 = g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore;
 constexpr int kW4MinK = 256;
 

@@ -298,12 +298,21 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
   }
 }
 
-// 128 x 64 tiles when 128 x 128 ones would give fewer than two workgroups
-// per CU (each CU then keeps two resident: one's barrier and fragment-read
-// latency hide behind the other's MFMAs)
-inline bool narrow_tiles(int M, int N) {
-  const int64_t t128 = (int64_t)((M + kBM - 1) / kBM) * ((N + 127) / 128);
-  return t128 < 2 * kNumCU && N > 64;
+// 128 x 64 tiles when they fill the chip's workgroup slots (occ per CU)
+// better than 128 x 128 ones: a grid of t tiles runs in ceil(t / slots)
+// rounds, and a last round that is mostly empty idles the CUs for a whole
+// tile's time.  4000 x 3000 f64 at 2 per CU: 768 square tiles = 1.5 rounds
+// (0.75 of the slots busy) vs 1504 narrow ones = 2.94 (0.98) -- 66% of
+// torch.matmul before (profiles/r5_gemm_fp_bench.jsonl).  Small products
+// (2048^2: 256 square tiles, one half-empty round) go narrow the same way.
+inline double round_fill(int64_t tiles, int64_t slots) {
+  const int64_t rounds = (tiles + slots - 1) / slots;
+  return rounds > 0 ? (double)tiles / (double)(rounds * slots) : 1.0;
+}
+inline bool narrow_tiles(int M, int N, int occ) {
+  if (N <= 64) return false;
+  const int64_t tm = (M + kBM - 1) / kBM, slots = (int64_t)occ * kNumCU;
+  return round_fill(tm * ((N + 63) / 64), slots) > round_fill(tm * ((N + 127) / 128), slots) + 0.05;
 }
 
 // Tile shape and depth.  BK_GEMM_FP_BN (64 | 128) and BK_GEMM_FP_BK (a K
@@ -313,11 +322,12 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
             hipStream_t stream) {
   const char* ebn = getenv("BK_GEMM_FP_BN");
   const char* ebk = getenv("BK_GEMM_FP_BK");
-  const bool nar = ebn ? atoi(ebn) == 64 : narrow_tiles(M, N);
   // f32: a 64-byte K tile (16 deep) halves the LDS a workgroup holds, so a
   // CU keeps three of them resident (its registers allow it) instead of two
   const int bk_default = std::is_same<T, float>::value ? 16 : Cfg<T>::kDefaultBK;
   const int bk = ebk ? atoi(ebk) : bk_default;
+  const int occ = std::is_same<T, float>::value && bk == 16 ? 3 : 2;
+  const bool nar = ebn ? atoi(ebn) == 64 : narrow_tiles(M, N, occ);
   const int bn = nar ? 64 : 128;
   const unsigned grid = (unsigned)(((M + kBM - 1) / kBM) * ((N + bn - 1) / bn));
   // vector fragment reads (BK_GEMM_FP_VEC=1): measured no faster on MI355X

@@ -149,7 +149,7 @@ BK_API int bk_rand_uniform(void* out, int64_t n, int dtype, uint64_t seed, uint6
   // the f64 / f32 draws take a 4x larger grid cap than the elementwise
   // kernels: 1e8 f64 (800 MB), rocprofv3 mean / min: 64 blocks/CU 146 / 139
   // us, 128: 133 / 118, 256: 133 / 121, 512: 130 / 115
-  // (profiles/r3_philox_grid_sweep.log)
+  // (profiles/archive/r3_philox_grid_sweep.log)
   constexpr int kDrawBlocksPerCU = 256;
   if (dtype == kF64) {
     const int64_t pairs = (n + 1) / 2;

@@ -43,8 +43,8 @@ constexpr int kRedMaxBlocks = 32768;
 // tools/reduce_sweep.py on MI355X, 1e8 f64 square-sum, median of 20 --
 // grid-stride layout 167 / 135 / 141 / 154 / 164 / 178 us at 256 / 512 / 768 /
 // 1024 / 2048 / 4096 blocks, block-contiguous 168 / 142 / 145 / 145 / 157 /
-// 158; torch.sum over the same 800 MB 139 us (profiles/r4_reduce_sweep*.jsonl;
-// the old 8192-block grid: 175-178 us).  Round 4 (profiles/r4_reduce_layout_sweep.jsonl,
+// 158; torch.sum over the same 800 MB 139 us (profiles/archive/r4_reduce_sweep*.jsonl;
+// the old 8192-block grid: 175-178 us).  Round 4 (profiles/archive/r4_reduce_layout_sweep.jsonl,
 // interleaved): the LDS-DMA stream below 140-145 us at its best grid (256
 // blocks), the same as this kernel at 512; 4 or 8 loads in flight per lane
 // instead of 16 at 512 / 1024 / 2048 blocks: 137.7 / 164-167 / 166-172 us --
@@ -53,10 +53,10 @@ constexpr int kRedMaxBlocks = 32768;
 constexpr int kRedBlocks = 512;
 constexpr int kRedUnroll = 16;
 // the fused RNG->reduce kernels are VALU-bound (80% of SIMD cycles issue
-// VALU, profiles/r4_payload_kernels_pmc.csv): 8 blocks per CU (8 waves per
+// VALU, profiles/archive/r4_payload_kernels_pmc.csv): 8 blocks per CU (8 waves per
 // SIMD) hide more of each Philox chain's latency -- 1e8 f64 square-sum
 // 91.3-91.5 us at 1024 blocks, 89.3-89.5 at 2048, 89.9-90.8 at 3072,
-// 90.5-91.2 at 4096, 101.9 at 8192 (profiles/r4_rand_reduce_sweep.jsonl)
+// 90.5-91.2 at 4096, 101.9 at 8192 (profiles/archive/r4_rand_reduce_sweep.jsonl)
 constexpr int kRandRedMaxBlocks = 2048;
 
 // lab overrides of grid targets (positive integers; anything else = default)
@@ -313,9 +313,9 @@ __global__ __launch_bounds__(kRedBlock) void reduce_chunked(const T* __restrict_
 // landed.  MI355X_MICROARCH.md measures an LDS-DMA stream at 6.4 TB/s
 // (6.5-6.8 nt) against ~6.3 for register-staged copies; the register-load
 // kernels above reach 5.7 TB/s on this reduction (torch.sum 5.8,
-// profiles/r4_reduce_sweep3.jsonl).  Measured, it does not beat them: 144-145
+// profiles/archive/r4_reduce_sweep3.jsonl).  Measured, it does not beat them: 144-145
 // us per-wave contiguous, 139-141 us with grid-strided pieces (STRIDED), both
-// at 256 blocks; slower at 512+ (profiles/r4_reduce_layout_sweep.jsonl).  A lab
+// at 256 blocks; slower at 512+ (profiles/archive/r4_reduce_layout_sweep.jsonl).  A lab
 // layout (BK_REDUCE_LAYOUT=ldsdma / ldsdma_stride), exact against fp64 numpy
 // (tools/probe/reduce_layout_check.py).  Only the issuing wave reads a slot, so
 // no barrier orders the ring: vmcnt before the read, lgkmcnt(0) before the
@@ -697,7 +697,7 @@ int launch_axis(const T* x, int64_t rows, int64_t cols, int64_t ld, int axis, TO
   // 16-wave vector kernel at ~128 blocks of >= 1024 rows (a block that
   // streams only 2 steps is mostly block start-up, ticket and fold).  4096^2
   // bf16, rocprofv3 min: 1024 blocks x 128 rows 14.2 us, 256 x 512 10.6,
-  // 128 x 1024 9.4 (profiles/r3_colsum_chunking_sweep.log,
+  // 128 x 1024 9.4 (profiles/archive/r3_colsum_chunking_sweep.log,
   // tools/probe/axis_shapes.py).  BK_COLSUM_BLOCKS / BK_COLSUM_MIN_ROWS
   // override the vector targets (lab sweeps).
   static const int64_t vec_blocks = env_int("BK_COLSUM_BLOCKS", 128);
