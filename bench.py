@@ -31,6 +31,7 @@ import gc
 import json
 import math
 import os
+import shutil
 import socket
 import statistics
 import subprocess
@@ -1146,6 +1147,8 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         loop.close()
+        # the service's sandbox tree lives in /dev/shm (memory): gone with the run
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 if __name__ == "__main__":

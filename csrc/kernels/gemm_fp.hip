@@ -302,17 +302,23 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
 // better than 128 x 128 ones: a grid of t tiles runs in ceil(t / slots)
 // rounds, and a last round that is mostly empty idles the CUs for a whole
 // tile's time.  4000 x 3000 f64 at 2 per CU: 768 square tiles = 1.5 rounds
-// (0.75 of the slots busy) vs 1504 narrow ones = 2.94 (0.98) -- 66% of
-// torch.matmul before (profiles/r5_gemm_fp_bench.jsonl).  Small products
-// (2048^2: 256 square tiles, one half-empty round) go narrow the same way.
+// (0.75 of the slots busy) vs 1504 narrow ones = 2.94 (0.98): 66% -> 74% of
+// torch.matmul (profiles/r5_gemm_fp_bench.jsonl, r5_gemm_fp_tiles.jsonl).
+// Small products (fewer square tiles than two per CU) always go narrow.
 inline double round_fill(int64_t tiles, int64_t slots) {
   const int64_t rounds = (tiles + slots - 1) / slots;
   return rounds > 0 ? (double)tiles / (double)(rounds * slots) : 1.0;
 }
 inline bool narrow_tiles(int M, int N, int occ) {
   if (N <= 64) return false;
-  const int64_t tm = (M + kBM - 1) / kBM, slots = (int64_t)occ * kNumCU;
-  return round_fill(tm * ((N + 63) / 64), slots) > round_fill(tm * ((N + 127) / 128), slots) + 0.05;
+  const int64_t tm = (M + kBM - 1) / kBM, t128 = tm * ((N + 127) / 128);
+  if (t128 < 2 * kNumCU) return true;
+  // the round model holds at two per CU; at three (f32) a short last round
+  // runs its workgroups faster, and narrow tiles lost: 4096^3 f32 0.84 vs
+  // 0.88 of torch.matmul with square ones (gpurun_out r5 bench 6 vs 4)
+  if (occ > 2) return false;
+  const int64_t slots = (int64_t)occ * kNumCU;
+  return round_fill(tm * ((N + 63) / 64), slots) > round_fill(t128, slots) + 0.05;
 }
 
 // Tile shape and depth.  BK_GEMM_FP_BN (64 | 128) and BK_GEMM_FP_BK (a K
