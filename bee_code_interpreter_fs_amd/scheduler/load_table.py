@@ -1,10 +1,10 @@
 """Read side of an executor daemon's load table (``LoadTable`` in
-csrc/executor/sandbox.hpp).
+csrc/executor/admission.hpp).
 
 Every front-end replica of a node routes Executes to the node's per-GPU
 executor daemons.  Admission itself -- the in-flight bound and the HBM
 commitment -- is enforced by each daemon for all replicas at once
-(``sandbox.cpp`` run_job); this table is what lets a replica *route* by the
+(``admission.cpp``); this table is what lets a replica *route* by the
 node-wide load (admitted + waiting jobs, committed HBM, gang reservations)
 rather than by the requests it happens to have sent itself.  The daemon
 publishes it in a 4 KiB shared file under its private run directory; a
@@ -52,8 +52,16 @@ class LoadTable:
             self._map = mmap.mmap(fd, 4096, mmap.MAP_SHARED, mmap.PROT_READ)
         finally:
             os.close(fd)
+        self._last: Optional[Load] = None
 
     def read(self) -> Optional[Load]:
+        """The daemon's current load, or -- when every try saw a write in
+        progress (a writer descheduled between its two sequence bumps, on a
+        crowded host) -- the last load read.  Never "no table" for a torn
+        read: routing treats a slot without a table as holding only this
+        replica's requests, so a slot whose reads kept tearing drew more
+        work (the 8-slot rehearsal once gave one slot 335 executions against
+        ~220 for the others)."""
         for _ in range(64):
             seq0 = struct.unpack_from("<Q", self._map, 8)[0]
             if seq0 & 1:
@@ -63,9 +71,10 @@ class LoadTable:
                 continue
             if vals[0] != MAGIC:
                 return None
-            return Load(vals[2], vals[3], vals[4], vals[5], vals[6], bool(vals[7]), vals[8], vals[9], vals[10],
-                        vals[11])
-        return None
+            self._last = Load(vals[2], vals[3], vals[4], vals[5], vals[6], bool(vals[7]), vals[8], vals[9], vals[10],
+                              vals[11])
+            return self._last
+        return self._last
 
     def close(self) -> None:
         try:

@@ -610,3 +610,30 @@ def test_wait_warm_accepts_a_disabled_warm_gang_set():
     assert asyncio.run(backend("ready").wait_warm(1.0)) is True
     assert asyncio.run(backend("disabled").wait_warm(1.0)) is True
     assert asyncio.run(backend("warming").wait_warm(0.3)) is False
+
+
+def test_load_table_torn_read_keeps_the_last_load(tmp_path):
+    """A reader that only ever sees a write in progress (odd seq) returns
+    the last load it read, not "no table" -- which routing would take for
+    an idle GPU (scheduler/load_table.py)."""
+    import struct
+
+    from bee_code_interpreter_fs_amd.scheduler import load_table as lt
+
+    path = tmp_path / "load"
+    vals = [lt.MAGIC, 2, 3, 1, 5 << 20, 8, 40 << 30, 0, 17, 1234, 4, 6 << 20]
+    path.write_bytes(struct.pack(lt._FMT, *vals).ljust(4096, b"\0"))
+    t = lt.open_table(str(path))
+    got = t.read()
+    assert got is not None and (got.jobs, got.waiting, got.executions, got.depth) == (3, 1, 17, 4)
+    with open(path, "r+b") as f:  # the writer stops between its two seq bumps
+        f.seek(8)
+        f.write(struct.pack("<Q", 3))
+        f.seek(16)
+        f.write(struct.pack("<q", 7))  # (a half-written jobs count)
+    again = t.read()
+    assert again is not None and again.jobs == 3 and again.executions == 17
+    with open(path, "r+b") as f:  # a table that is not (or no longer) one
+        f.write(struct.pack("<QQ", 0, 4))
+    assert t.read() is None
+    t.close()
