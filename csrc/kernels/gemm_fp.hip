@@ -332,7 +332,14 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   // CU keeps three of them resident (its registers allow it) instead of two
   const int bk_default = std::is_same<T, float>::value ? 16 : Cfg<T>::kDefaultBK;
   const int bk = ebk ? atoi(ebk) : bk_default;
-  const int occ = std::is_same<T, float>::value && bk == 16 ? 3 : 2;
+  // f32 at 16 deep: three workgroups per CU.  Four fit too (<= 128 VGPRs,
+  // 38 KiB of LDS each; not A . B^T, whose [n][k] B reads then spill), but
+  // measured level with three: 4096^3 0.884 vs 0.885 of torch.matmul, 8192^3
+  // 0.881 both (profiles/r5_gemm_fp_occ.jsonl) -- the waves' fragment-read
+  // waits after each barrier, not the slot count, hold it.  BK_GEMM_FP_OCC=4.
+  const char* eocc = getenv("BK_GEMM_FP_OCC");
+  constexpr bool kOcc4 = !(!TA && TB);
+  const int occ = std::is_same<T, float>::value && bk == 16 ? (kOcc4 && eocc && atoi(eocc) == 4 ? 4 : 3) : 2;
   const bool nar = ebn ? atoi(ebn) == 64 : narrow_tiles(M, N, occ);
   const int bn = nar ? 64 : 128;
   const unsigned grid = (unsigned)(((M + kBM - 1) / kBM) * ((N + bn - 1) / bn));
@@ -342,8 +349,9 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   const bool vf = getenv("BK_GEMM_FP_VEC") && atoi(getenv("BK_GEMM_FP_VEC")) != 0;
 #define BK_FP_LAUNCH(V, W, D, O)                                                                              \
   do {                                                                                                        \
-    if (vf && std::is_same<T, float>::value)                                                                  \
-      gemm_fp_kernel<T, TA, TB, V, W, D, O, std::is_same<T, float>::value><<<grid, kThreads, 0, stream>>>(     \
+    if (vf && std::is_same<T, float>::value && (O) < 4) /* (at four per CU the vector reads spill) */          \
+      gemm_fp_kernel<T, TA, TB, V, W, D, O, std::is_same<T, float>::value && (O) < 4><<<grid, kThreads, 0,       \
+                                                                                     stream>>>(                \
           (const T*)A, (const T*)B, (T*)C, M, N, K, lda, ldb, ldc);                                             \
     else                                                                                                      \
       gemm_fp_kernel<T, TA, TB, V, W, D, O, false><<<grid, kThreads, 0, stream>>>((const T*)A, (const T*)B,     \
@@ -361,7 +369,10 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
       BK_FP_LAUNCH(false, 128, D, O); \
   } while (0)
   if constexpr (std::is_same<T, float>::value) {
-    if (bk == 16)
+    constexpr int kHigh = kOcc4 ? 4 : 3;
+    if (kOcc4 && bk == 16 && occ == 4)
+      BK_FP_DEPTH(16, kHigh);
+    else if (bk == 16)
       BK_FP_DEPTH(16, 3);
     else
       BK_FP_DEPTH(32, 2);
