@@ -91,10 +91,10 @@ class HipDevice final : public broker::Device {
   // whole wait even under hipDeviceScheduleBlockingSync (measured on MI355X,
   // tools/probe/sync_cpu_probe.hip: a 150 us kernel cost 159 us of CPU in
   // hipStreamSynchronize, 7 us this way), and every reduce / read of every
-  // sandbox waits.  Checks 2 us apart at first, then each 1/8 of the time
-  // waited so far after the last (<= 50 us; the broker threads run with a
+  // sandbox waits.  Checks 2 us apart at first, then each 1/4 of the time
+  // waited so far after the last (<= 500 us; the broker threads run with a
   // 1 us timer slack): the checks grow geometrically and a wait overshoots by
-  // at most 1/8.  BEE_BROKER_POLL tunes it, BEE_BROKER_WAIT=spin: HIP's wait.
+  // at most 1/4.  BEE_BROKER_POLL tunes it, BEE_BROKER_WAIT=spin: HIP's wait.
   bool wait(Ctx* c) {
     if (spin_wait_) return hipStreamSynchronize(c->s) == hipSuccess;
     if (!c->wait_ev && hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming) != hipSuccess)
@@ -427,8 +427,12 @@ class HipDevice final : public broker::Device {
   // of its length either way, and the long waits of a crowded GPU (8 slots
   // folded onto one card: ~10 ms in-sandbox) no longer cost a check every
   // 50 us -- 200 wake-ups per 10 ms wait, on every waiting session.
+  // Round 5: each check 1/4 of the wait so far after the last (was 1/8):
+  // 600-step headline A/B, 2 interleaved rounds on one box, daemon CPU
+  // 0.665 / 0.673 vs 0.700 / 0.690 ms per Execute, RPS 3328 / 3280 vs 3300 /
+  // 3247; 1/2 lost throughput (3092 / 3185) (profiles/r5_broker_poll_ab.jsonl).
   long poll_min_ns_ = 2000, poll_max_ns_ = 500000;
-  int poll_div_ = 8;
+  int poll_div_ = 4;
   bool poll_set_ = (poll_schedule(&poll_min_ns_, &poll_max_ns_, &poll_div_), true);
   void* lib_ = nullptr;
   std::string arch_;

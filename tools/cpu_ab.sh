@@ -2,7 +2,8 @@
 # Interleaved A/B of service-side CPU knobs on the headline bench (one box):
 # each variant is an environment for the whole service (daemons, zygotes,
 # sandboxes inherit it); every run appends its JSON line, labelled, to
-# gpurun_out/cpu_ab.jsonl.  Variants: "name=VAR=val,VAR=val" ("base" = none).
+# gpurun_out/cpu_ab.jsonl.  Variants: "name=VAR=val;VAR=val" ("base" = none;
+# values may hold commas).
 #   bash tools/cpu_ab.sh STEPS ROUNDS base "nosetsid=BEE_SANDBOX_SETSID=0" ...
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -14,7 +15,7 @@ for round in $(seq 1 $ROUNDS); do
     vars=""
     [ "$spec" != "$name" ] && vars=${spec#*=}
     envs=()
-    IFS=',' read -ra kvs <<< "$vars"
+    IFS=';' read -ra kvs <<< "$vars"
     for kv in "${kvs[@]}"; do [ -n "$kv" ] && envs+=("$kv"); done
     echo "[cpu_ab] round $round $name ${envs[*]}" >&2
     line=$(env "${envs[@]}" timeout -k 10 300 python3 $R/bench.py --gpus 1 --steps $STEPS --warmup 20 2>>$R/gpurun_out/cpu_ab.err | grep '^{' | tail -1)
