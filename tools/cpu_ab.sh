@@ -3,7 +3,7 @@
 # each variant is an environment for the whole service (daemons, zygotes,
 # sandboxes inherit it); every run appends its JSON line, labelled, to
 # gpurun_out/cpu_ab.jsonl.  Variants: "name=VAR=val;VAR=val" ("base" = none;
-# values may hold commas).
+# values may hold commas; ARGS=--flag+value adds bench.py arguments).
 #   bash tools/cpu_ab.sh STEPS ROUNDS base "nosetsid=BEE_SANDBOX_SETSID=0" ...
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -16,9 +16,13 @@ for round in $(seq 1 $ROUNDS); do
     [ "$spec" != "$name" ] && vars=${spec#*=}
     envs=()
     IFS=';' read -ra kvs <<< "$vars"
-    for kv in "${kvs[@]}"; do [ -n "$kv" ] && envs+=("$kv"); done
+    extra=()
+    for kv in "${kvs[@]}"; do
+      if [ "${kv%%=*}" = "ARGS" ]; then read -ra extra <<< "${kv#ARGS=}"; extra=("${extra[@]//+/ }");  # ARGS=--frontends+2
+      elif [ -n "$kv" ]; then envs+=("$kv"); fi
+    done
     echo "[cpu_ab] round $round $name ${envs[*]}" >&2
-    line=$(env "${envs[@]}" timeout -k 10 300 python3 $R/bench.py --gpus 1 --steps $STEPS --warmup 20 2>>$R/gpurun_out/cpu_ab.err | grep '^{' | tail -1)
+    line=$(env "${envs[@]}" timeout -k 10 300 python3 $R/bench.py --gpus 1 --steps $STEPS --warmup 20 ${extra[*]} 2>>$R/gpurun_out/cpu_ab.err | grep '^{' | tail -1)
     rc=$?
     if [ $rc -ne 0 ] || [ -z "$line" ]; then echo "[cpu_ab] $name failed rc=$rc" >&2; exit 1; fi
     python3 -c "
