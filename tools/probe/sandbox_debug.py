@@ -45,7 +45,7 @@ def main():
     try:
         for i in range(args.n):
             r = h.call(h.ctx.code_executor.execute(source_code=src), timeout=300)
-            lines = [l for l in r.stderr.splitlines() if l.startswith(("NEW_MODULES", "STAMPS"))]
+            lines = [l for l in r.stderr.splitlines() if l.startswith(("NEW_MODULES", "STAMPS", "TEARDOWN"))]
             print(json.dumps({"i": i, "exit": r.exit_code, "debug": lines,
                               "timings": {k: round(v, 3) for k, v in sorted(r.timings_ms.items())}}), flush=True)
     finally:
