@@ -8,6 +8,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 STEPS=$1; ROUNDS=$2; shift 2
+WARMUP=${WARMUP:-20}  # WARMUP=5 with STEPS=20: the driver's command
 OUT=$R/gpurun_out/cpu_ab.jsonl
 for round in $(seq 1 $ROUNDS); do
   for spec in "$@"; do
@@ -22,7 +23,7 @@ for round in $(seq 1 $ROUNDS); do
       elif [ -n "$kv" ]; then envs+=("$kv"); fi
     done
     echo "[cpu_ab] round $round $name ${envs[*]}" >&2
-    line=$(env "${envs[@]}" timeout -k 10 300 python3 $R/bench.py --gpus 1 --steps $STEPS --warmup 20 ${extra[*]} 2>>$R/gpurun_out/cpu_ab.err | grep '^{' | tail -1)
+    line=$(env "${envs[@]}" timeout -k 10 300 python3 $R/bench.py --gpus 1 --steps $STEPS --warmup $WARMUP ${extra[*]} 2>>$R/gpurun_out/cpu_ab.err | grep '^{' | tail -1)
     rc=$?
     if [ $rc -ne 0 ] || [ -z "$line" ]; then echo "[cpu_ab] $name failed rc=$rc" >&2; exit 1; fi
     python3 -c "
