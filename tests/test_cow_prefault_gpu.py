@@ -1,0 +1,55 @@
+"""The copy-on-write prefault on the MI355X box, where the service runs
+unprivileged: the learner sandbox can read its pagemap only once the jail
+has made it dumpable (csrc/zygote/zygote_loop.cpp cow_report), so this is
+the path the CPU test (root, tests/test_cow_prefault_cpu.py) cannot cover.
+Headline payload, one client."""
+
+import json
+import os
+import tempfile
+
+import pytest
+
+from .harness import ServiceHarness, ensure_native_executor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _stamps(stderr: str) -> dict:
+    for line in stderr.splitlines():
+        if line.startswith("STAMPS "):
+            return json.loads(line[len("STAMPS "):])
+    return {}
+
+
+@pytest.mark.gpu
+def test_learners_read_their_pagemap_and_later_sandboxes_prefault():
+    ensure_native_executor()
+    saved = {k: os.environ.get(k) for k in ("BEE_DEBUG_NEW_MODULES", "BEE_COW_RELEARN")}
+    os.environ.update({"BEE_DEBUG_NEW_MODULES": "1", "BEE_COW_RELEARN": "16"})
+    tmp = tempfile.mkdtemp(prefix="bee-cow-", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    h = ServiceHarness(tmp, gpu_ids=[0], workers_per_gpu_target=0, min_workers_per_gpu_target=2,
+                       light_workers_per_gpu_target=0, default_timeout=120.0)
+    try:
+        h.start()
+        src = open(os.path.join(ROOT, "examples", "benchmark_numpy_gpu.py")).read()
+        rows = []
+        for _ in range(24):
+            r = h.call(h.ctx.code_executor.execute(source_code=src), timeout=300)
+            assert r.exit_code == 0 and "Result:" in r.stdout, r.stderr
+            rows.append(_stamps(r.stderr))
+        learners = [s for s in rows if "cow_learned_pages" in s]
+        assert learners, [sorted(s)[:5] for s in rows[:2]]
+        assert all(s["cow_pagemap_open"] for s in learners), learners
+        assert max(s["cow_learned_pages"] for s in learners) >= 50, learners
+        assert sum(1 for s in rows if s.get("cow_prefault_pages", 0) > 0) >= len(rows) // 2, rows
+    finally:
+        h.stop()
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        import shutil
+
+        shutil.rmtree(tmp, ignore_errors=True)
