@@ -389,16 +389,33 @@ constexpr uint64_t kPage = 4096;
 #define MADV_POPULATE_WRITE 23
 #endif
 
-struct CowState {
-  int mode = -1;                 // 0 off, 1 the request path's pages, 2 every page a sandbox writes
-  uint64_t relearn = 1024;       // forks between learners
-  std::vector<Run> hot;          // zygote: the learned runs
+// A zygote forks sandboxes of more than one kind -- the nano zygote both
+// beekern scripts' sandboxes and, with a lazy broker session
+// (BEE_BROKER_LAZY=1 in the spawn line), stdlib-only scripts' -- whose
+// request paths write different pages: a set learned from one kind made the
+// other copy pages it never touched (hello_world on a GPU pod, one shared
+// set learned from the self-warm's beekern payload: pooled CPU 1.58-1.82 vs
+// 1.32-1.34 ms per sandbox without the prefault).  So each spawn profile
+// learns and prefaults its own set (then: hello 1.59-1.63 vs 1.34-1.42 ms,
+// the request path's own pages; headline 3294 / 3260 vs 3010 / 3008 RPS,
+// profiles/r5_cow_profiles_ab.jsonl).
+constexpr int kCowProfiles = 2;  // 0: eager broker session, 1: lazy (BEE_BROKER_LAZY=1)
+
+struct CowProfile {
+  std::vector<Run> hot;          // the learned runs
   uint64_t hot_pages = 0;
   uint64_t forks_since = 0;      // forks since the last set arrived
-  int learn_rd = -1;             // zygote: the outstanding learner's pipe
+  int learn_rd = -1;             // the outstanding learner's pipe
   std::string learn_buf;
   uint64_t sets = 0;             // sets learned so far
+};
+
+struct CowState {
+  int mode = -1;                 // 0 off, 1 the request path's pages, 2 every page a sandbox writes
+  uint64_t relearn = 1024;       // forks (of a profile) between learners
+  CowProfile prof[kCowProfiles];
   // in a child
+  int profile = 0;
   int learn_wr = -1;
   std::vector<Run> entry;        // learner: private writable mappings at entry
   std::vector<uint64_t> mark;    // learner (mode 1): the pages it held when its request came
@@ -406,6 +423,11 @@ struct CowState {
   uint64_t prefault_pages = 0;
   double prefault_ms = 0;
 } g_cow;
+
+// the spawn line's profile (the executor's own compact JSON)
+int cow_profile_of(const std::string& line) {
+  return line.find("\"BEE_BROKER_LAZY\":\"1\"") != std::string::npos ? 1 : 0;
+}
 
 void cow_config() {
   if (g_cow.mode >= 0) return;
@@ -435,24 +457,25 @@ void private_writable_maps(std::vector<Run>* out) {
   fclose(f);
 }
 
-// zygote, after forking a learner
-void cow_parent_learner(int rd) {
-  g_cow.learn_rd = rd;
-  g_cow.learn_buf.clear();
+// zygote, after forking a learner of profile p
+void cow_parent_learner(int p, int rd) {
+  g_cow.prof[p].learn_rd = rd;
+  g_cow.prof[p].learn_buf.clear();
 }
 
-// zygote: the learner's pipe is readable; true once it is closed
-bool cow_parent_read() {
+// zygote: profile p's learner pipe is readable; true once it is closed
+bool cow_parent_read(int p) {
+  CowProfile& pr = g_cow.prof[p];
   char tmp[65536];
-  const ssize_t n = read(g_cow.learn_rd, tmp, sizeof tmp);
+  const ssize_t n = read(pr.learn_rd, tmp, sizeof tmp);
   if (n < 0 && (errno == EINTR || errno == EAGAIN)) return false;
   if (n > 0) {
-    if (g_cow.learn_buf.size() + (size_t)n <= 16 + kCowMaxRuns * sizeof(Run)) g_cow.learn_buf.append(tmp, (size_t)n);
+    if (pr.learn_buf.size() + (size_t)n <= 16 + kCowMaxRuns * sizeof(Run)) pr.learn_buf.append(tmp, (size_t)n);
     return false;
   }
-  close(g_cow.learn_rd);
-  g_cow.learn_rd = -1;
-  const std::string& s = g_cow.learn_buf;
+  close(pr.learn_rd);
+  pr.learn_rd = -1;
+  const std::string& s = pr.learn_buf;
   uint64_t hdr[2];
   if (s.size() >= sizeof hdr) {
     memcpy(hdr, s.data(), sizeof hdr);
@@ -477,47 +500,52 @@ bool cow_parent_read() {
         pages += (r.b - r.a) / kPage;
         got.push_back(r);
       }
-      g_cow.hot.swap(got);
-      g_cow.hot_pages = pages;
-      g_cow.forks_since = 0;
-      g_cow.sets++;
+      pr.hot.swap(got);
+      pr.hot_pages = pages;
+      pr.forks_since = 0;
+      pr.sets++;
     }
   }
-  g_cow.learn_buf.clear();
-  g_cow.learn_buf.shrink_to_fit();
+  pr.learn_buf.clear();
+  pr.learn_buf.shrink_to_fit();
   return true;
 }
 
-// zygote, before a fork: should this child learn?  (opens its pipe)
-bool cow_want_learner(int p[2]) {
+// zygote, before a fork of profile p: should this child learn?  (opens its pipe)
+bool cow_want_learner(int p, int fds[2]) {
   if (g_cow.mode == 0) return false;
-  if (g_cow.learn_rd >= 0) {
+  CowProfile& pr = g_cow.prof[p];
+  if (pr.learn_rd >= 0) {
     // a learner that never answers (its request never came, or a descendant
     // holds the pipe): give up on it after a while
-    if (++g_cow.forks_since < 4 * g_cow.relearn) return false;
-    close(g_cow.learn_rd);
-    g_cow.learn_rd = -1;
+    if (++pr.forks_since < 4 * g_cow.relearn) return false;
+    close(pr.learn_rd);
+    pr.learn_rd = -1;
   } else {
-    ++g_cow.forks_since;
+    ++pr.forks_since;
   }
-  if (!g_cow.hot.empty() && g_cow.forks_since < g_cow.relearn) return false;
-  return pipe2(p, O_CLOEXEC) == 0;
+  if (!pr.hot.empty() && pr.forks_since < g_cow.relearn) return false;
+  return pipe2(fds, O_CLOEXEC) == 0;
 }
 
-// in a fresh child: learn (with the pipe's write end) or prefault the set
-void cow_child(int learn_wr) {
-  if (g_cow.learn_rd >= 0) {  // the zygote's end of another learner's pipe
-    close(g_cow.learn_rd);
-    g_cow.learn_rd = -1;
-  }
+// in a fresh child of profile p: learn (with the pipe's write end) or
+// prefault that profile's set
+void cow_child(int p, int learn_wr) {
+  for (CowProfile& pr : g_cow.prof)
+    if (pr.learn_rd >= 0) {  // the zygote's ends of learner pipes
+      close(pr.learn_rd);
+      pr.learn_rd = -1;
+    }
+  g_cow.profile = p;
   if (learn_wr >= 0) {
     g_cow.learn_wr = learn_wr;
     private_writable_maps(&g_cow.entry);  // (maps is 0444: readable while non-dumpable)
     return;
   }
-  if (g_cow.mode == 0 || g_cow.hot.empty()) return;
+  const CowProfile& pr = g_cow.prof[p];
+  if (g_cow.mode == 0 || pr.hot.empty()) return;
   const double t0 = mono_s();
-  for (const Run& r : g_cow.hot) {
+  for (const Run& r : pr.hot) {
     if (madvise((void*)r.a, r.b - r.a, MADV_POPULATE_WRITE) == 0) {
       g_cow.prefault_pages += (r.b - r.a) / kPage;
     } else if (errno == EINVAL) {
@@ -594,10 +622,11 @@ PyObject* cow_report(PyObject*, PyObject*) {
 }
 
 PyObject* cow_stats(PyObject*, PyObject*) {
-  return Py_BuildValue("{s:i,s:n,s:K,s:K,s:d,s:O,s:K}", "mode", g_cow.mode, "hot_runs", (Py_ssize_t)g_cow.hot.size(),
-                       "hot_pages", (unsigned long long)g_cow.hot_pages, "prefault_pages",
+  const CowProfile& pr = g_cow.prof[g_cow.profile];
+  return Py_BuildValue("{s:i,s:i,s:n,s:K,s:K,s:d,s:O,s:K}", "mode", g_cow.mode, "profile", g_cow.profile, "hot_runs",
+                       (Py_ssize_t)pr.hot.size(), "hot_pages", (unsigned long long)pr.hot_pages, "prefault_pages",
                        (unsigned long long)g_cow.prefault_pages, "prefault_ms", g_cow.prefault_ms, "learner",
-                       g_cow.learn_wr >= 0 ? Py_True : Py_False, "sets", (unsigned long long)g_cow.sets);
+                       g_cow.learn_wr >= 0 ? Py_True : Py_False, "sets", (unsigned long long)pr.sets);
 }
 
 // ---- native sandbox bootstrap ----------------------------------------------
@@ -1016,8 +1045,10 @@ PyObject* serve(PyObject*, PyObject* args) {
 
   cow_config();
   while (!stop) {
-    pollfd fds[3] = {{chan, POLLIN, 0}, {sfd, POLLIN, 0}, {g_cow.learn_rd, POLLIN, 0}};
-    const int pr = poll(fds, g_cow.learn_rd >= 0 ? 3 : 2, 1000);
+    // (a negative descriptor is skipped by poll: a profile without a learner out)
+    pollfd fds[2 + kCowProfiles] = {{chan, POLLIN, 0}, {sfd, POLLIN, 0}};
+    for (int p = 0; p < kCowProfiles; ++p) fds[2 + p] = {g_cow.prof[p].learn_rd, POLLIN, 0};
+    const int pr = poll(fds, 2 + kCowProfiles, 1000);
     if (pr < 0) {
       if (errno == EINTR) continue;
       break;
@@ -1035,8 +1066,10 @@ PyObject* serve(PyObject*, PyObject* args) {
       reap();
     }
     if (stop) break;
-    if (fds[2].fd >= 0 && g_cow.learn_rd == fds[2].fd && (fds[2].revents & (POLLIN | POLLHUP | POLLERR)))
-      cow_parent_read();
+    for (int p = 0; p < kCowProfiles; ++p)
+      if (fds[2 + p].fd >= 0 && g_cow.prof[p].learn_rd == fds[2 + p].fd &&
+          (fds[2 + p].revents & (POLLIN | POLLHUP | POLLERR)))
+        cow_parent_read(p);
     if (fds[0].revents & (POLLIN | POLLHUP | POLLERR)) {
       char tmp[65536];
       const ssize_t n = read(chan, tmp, sizeof tmp);
@@ -1055,7 +1088,8 @@ PyObject* serve(PyObject*, PyObject* args) {
         top_level_string(line, "id", &id);
         const double t0 = mono_s();
         int lp[2] = {-1, -1};
-        const bool learner = cow_want_learner(lp);
+        const int prof = cow_profile_of(line);
+        const bool learner = cow_want_learner(prof, lp);
         const pid_t pid = fork();
         if (pid < 0) {
           const int e = errno;
@@ -1077,12 +1111,12 @@ PyObject* serve(PyObject*, PyObject* args) {
           sigprocmask(SIG_SETMASK, &old, nullptr);
           thp_child();
           if (learner) close(lp[0]);
-          cow_child(learner ? lp[1] : -1);
+          cow_child(prof, learner ? lp[1] : -1);
           return boot_child(line);
         }
         if (learner) {
           close(lp[1]);
-          cow_parent_learner(lp[0]);
+          cow_parent_learner(prof, lp[0]);
         }
         children.insert(pid);
         char ms[32];
