@@ -122,6 +122,11 @@ def _declare(lib: ctypes.CDLL) -> None:
         "bk_transpose_to_bf16": ([c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),
         "bk_transpose": ([c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),
         "bk_gemm_fp": ([c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_i64, c_i64, c_i64, c_vp], c_int),
+        "bk_gemm_f32x6_workspace_bytes": ([c_int, c_int, c_int], c_i64),
+        "bk_gemm_f32x6": (
+            [c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp],
+            c_int,
+        ),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -612,11 +612,36 @@ def _fp_dtype(x) -> bool:
     return x.dtype in ("float32", "float64")
 
 
+# f32 products take the six-piece bf16 split (csrc/kernels/gemm_fp.hip
+# bk_gemm_f32x6: f32-level error at the bf16 MFMA's rate) from 2^32
+# multiply-adds with M, N >= 256; smaller ones, and any product whose
+# workspace the HBM quota refuses, run on the f32 MFMA.  Measured medians
+# against the f32 kernel (profiles/r5_gemm_f32x6_bench.jsonl): 1024^3 80 vs
+# 51 us, 1536^3 113 vs 115, 2048^3 153 vs 156, 4096^3 785 vs 1044,
+# 8192^3 5905 vs 8126.  BEE_GEMM_F32X6: auto | 1 (whenever the shape allows)
+# | 0 (never).
+_F32X6 = os.environ.get("BEE_GEMM_F32X6", "auto")
+_F32X6_MIN_MACS = 1 << 32
+
+
+def f32x6_workspace_bytes(M: int, N: int, K: int) -> int:
+    """Workspace of the split product: a 256-byte header, then A' [M][6 Kp]
+    and B' [N][6 Kp] in bf16, Kp = K rounded up to 64 (broker_core.hpp)."""
+    return 256 + 12 * ((K + 63) // 64 * 64) * (M + N)
+
+
+def _use_f32x6(M: int, N: int, K: int) -> bool:
+    if _F32X6 == "0" or 6 * ((K + 63) // 64 * 64) > (1 << 22):
+        return False
+    return _F32X6 == "1" or (min(M, N) >= 256 and M * N * K >= _F32X6_MIN_MACS)
+
+
 def matmul_fp(a, b) -> DeviceArray:
     """C = A @ B in numpy's precision: f64 operands on the f64 MFMA
     (``v_mfma_f64_16x16x4_f64``), f32 on the exact f32 MFMA
-    (``v_mfma_f32_16x16x4_f32``), mixed f32/f64 promoted to f64 as numpy
-    does (``csrc/kernels/gemm_fp.hip``).  numpy's 1-D rules: a 1-D ``a`` is
+    (``v_mfma_f32_16x16x4_f32``) or, for large products, on the bf16 MFMA
+    through the six-piece split (f32-level error, :func:`f32x6_workspace_bytes`),
+    mixed f32/f64 promoted to f64 as numpy does (``csrc/kernels/gemm_fp.hip``).  numpy's 1-D rules: a 1-D ``a`` is
     a row vector, a 1-D ``b`` a column, and that axis is dropped from the
     result.  ``.T`` views are read in place (no transpose pass)."""
     a = _as_operand(a)
@@ -646,7 +671,19 @@ def matmul_fp(a, b) -> DeviceArray:
     a_ptr = a._buf.ptr if ta else a.ptr  # type: ignore[union-attr]
     b_ptr = b._buf.ptr if tb else b.ptr  # type: ignore[union-attr]
     c = DeviceArray((M, N), dt)
-    driver().gemm_fp(DTYPE_CODES[dt], ta, tb, a_ptr, b_ptr, c.ptr, M, N, K, M if ta else K, K if tb else N, N)
+    lda, ldb = (M if ta else K), (K if tb else N)
+    ws = None
+    if dt == "float32" and _use_f32x6(M, N, K):
+        nbytes = f32x6_workspace_bytes(M, N, K)
+        try:
+            ws = DeviceArray((nbytes // 2,), "bfloat16")
+        except QuotaExceeded:
+            ws = None  # (no room for the split operands: the f32 MFMA needs none)
+    if ws is not None:
+        driver().gemm_f32x6(ta, tb, a_ptr, b_ptr, c.ptr, M, N, K, lda, ldb, N, ws.ptr, nbytes)
+        del ws  # (freed in stream order)
+    else:
+        driver().gemm_fp(DTYPE_CODES[dt], ta, tb, a_ptr, b_ptr, c.ptr, M, N, K, lda, ldb, N)
     return c.reshape(out_shape) if out_shape != (M, N) else c
 
 

@@ -113,6 +113,12 @@ class NativeDriver:
         check(self.lib.bk_gemm_fp(dt, int(ta), int(tb), _vp(A), _vp(B), _vp(C), M, N, K, lda, ldb, ldc, self.stream),
               "bk_gemm_fp")
 
+    def gemm_f32x6(self, ta, tb, A, B, C, M, N, K, lda, ldb, ldc, W, ws_bytes) -> None:
+        """The same f32 product on the bf16 MFMA through the six-piece split
+        (csrc/kernels/gemm_fp.hip bk_gemm_f32x6); W: ws_bytes of workspace."""
+        check(self.lib.bk_gemm_f32x6(int(ta), int(tb), _vp(A), _vp(B), _vp(C), M, N, K, lda, ldb, ldc, _vp(W), ws_bytes,
+                                     self.stream), "bk_gemm_f32x6")
+
     def reduce_axis(self, op: int, dt: int, x: int, y: int, rows: int, cols: int, ld: int, axis: int) -> None:
         if not self.axis_ws:
             self.axis_ws = self.malloc(self.lib.bk_reduce_axis_workspace_bytes())
@@ -410,6 +416,11 @@ class BrokerDriver:
     def gemm_fp(self, dt, ta, tb, A, B, C, M, N, K, lda, ldb, ldc) -> None:
         flags = (1 if ta else 0) | (2 if tb else 0)
         self._post(GEMM_FP, struct.pack("<IIQQQiiiiqqq", dt, flags, A, B, C, M, N, K, 0, lda, ldb, ldc))
+
+    def gemm_f32x6(self, ta, tb, A, B, C, M, N, K, lda, ldb, ldc, W, ws_bytes) -> None:
+        # flags bit 2: the split product; the workspace handle trails (broker_core.hpp kGemmFpSplit)
+        flags = (1 if ta else 0) | (2 if tb else 0) | 4
+        self._post(GEMM_FP, struct.pack("<IIQQQiiiiqqqQ", 0, flags, A, B, C, M, N, K, 0, lda, ldb, ldc, W))
 
     def reduce_axis(self, op, dt, x, y, rows, cols, ld, axis) -> None:
         self._post(REDUCE_AXIS, struct.pack("<IIQQqqqII", op, dt, x, y, rows, cols, ld, axis, 0))

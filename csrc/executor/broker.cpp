@@ -65,6 +65,8 @@ class HipDevice final : public broker::Device {
     int (*axis_ws_init)(void*, hipStream_t);
     int (*reduce_axis)(int, int, const void*, int64_t, int64_t, int64_t, int, void*, void*, hipStream_t);
     int (*gemm_fp)(int, int, int, const void*, const void*, void*, int, int, int, int64_t, int64_t, int64_t, hipStream_t);
+    int (*gemm_f32x6)(int, int, const void*, const void*, void*, int, int, int, int64_t, int64_t, int64_t, void*, int64_t,
+                      hipStream_t);
   } bk{};
 
   // Per-session GPU resources, pooled across sessions: a stream, the
@@ -175,6 +177,7 @@ class HipDevice final : public broker::Device {
     sym(lib_, "bk_reduce_axis", &bk.reduce_axis);
     sym(lib_, "bk_gemm_bf16_nn", &bk.gemm_nn);
     sym(lib_, "bk_gemm_fp", &bk.gemm_fp);
+    sym(lib_, "bk_gemm_f32x6", &bk.gemm_f32x6);
     return true;
   }
 
@@ -378,6 +381,11 @@ class HipDevice final : public broker::Device {
               int64_t ldb, int64_t ldc, void* s) override {
     if (!bk.gemm_fp) return broker::kBadArgument;
     return bk.gemm_fp((int)dt, ta, tb, A, B, C, M, N, K, lda, ldb, ldc, pick(s, short_gemm(M, N, K)));
+  }
+  int gemm_f32x6(bool ta, bool tb, const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                 int64_t ldc, void* ws, uint64_t ws_bytes, void* s) override {
+    if (!bk.gemm_f32x6) return broker::kBadArgument;
+    return bk.gemm_f32x6(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, ws, (int64_t)ws_bytes, pick(s, short_gemm(M, N, K)));
   }
   int transpose(int sdt, int ddt, const void* in, void* out, int rows, int cols, int ldi, int ldo, void* s) override {
     return bk.transpose(sdt, ddt, in, out, rows, cols, ldi, ldo,

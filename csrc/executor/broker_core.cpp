@@ -356,11 +356,14 @@ int32_t Session::dispatch(uint32_t op, const char* payload, uint64_t len, std::v
       const int32_t M = r.get<int32_t>(), N = r.get<int32_t>(), K = r.get<int32_t>();
       (void)r.get<int32_t>();
       const int64_t lda = r.get<int64_t>(), ldb = r.get<int64_t>(), ldc = r.get<int64_t>();
+      const bool split = (gflags & kGemmFpSplit) != 0;
+      const uint64_t W = split ? r.get<uint64_t>() : 0;
       if (!r.ok) return kProtocol;
       const bool ta = (gflags & 1) != 0, tb = (gflags & 2) != 0;
       uint64_t na, nb, nc;
-      Buf *ba = lookup(A), *bb = lookup(B), *bc = lookup(C);
-      if ((dt != 0 && dt != 1) || (gflags & ~3u) != 0 ||
+      Buf *ba = lookup(A), *bb = lookup(B), *bc = lookup(C), *bw = split ? lookup(W) : nullptr;
+      const uint64_t nw = split ? f32x6_workspace_bytes(M, N, K) : 0;
+      if ((dt != 0 && dt != 1) || (gflags & ~7u) != 0 || (split && (dt != 0 || !bw || nw == 0 || nw > bw->size)) ||
           !(ta ? matrix_bytes(K, M, lda, dtype_size(dt), &na) : matrix_bytes(M, K, lda, dtype_size(dt), &na)) ||
           !(tb ? matrix_bytes(N, K, ldb, dtype_size(dt), &nb) : matrix_bytes(K, N, ldb, dtype_size(dt), &nb)) ||
           !matrix_bytes(M, N, ldc, dtype_size(dt), &nc) || !ba || !bb || !bc || na > ba->size || nb > bb->size ||
@@ -368,6 +371,10 @@ int32_t Session::dispatch(uint32_t op, const char* payload, uint64_t len, std::v
         return kBadHandle;
       // C is only written: its untouched gaps (ldc > N) keep their scrub state
       if (!will_read(ba) || !will_read(bb) || !(ldc == N ? will_write(bc, 0, nc) : will_read(bc))) return kLaunchFailed;
+      if (split) {  // the workspace's first nw bytes are all written (a larger one is scrubbed first)
+        if (bw == ba || bw == bb || bw == bc || !will_write(bw, 0, nw)) return kBadHandle;
+        return dev_.gemm_f32x6(ta, tb, ba->ptr, bb->ptr, bc->ptr, M, N, K, lda, ldb, ldc, bw->ptr, nw, stream_);
+      }
       return dev_.gemm_fp(dt, ta, tb, ba->ptr, bb->ptr, bc->ptr, M, N, K, lda, ldb, ldc, stream_);
     }
     case kTranspose: {

@@ -34,6 +34,10 @@ enum Status : int32_t {
 };
 constexpr uint32_t kNoReply = 1;                   // request flag
 constexpr uint32_t kGemmNN = 1;                    // GEMM payload flags: B stored [K][N]
+// GEMM_FP payload flags: 1 = A given as [K][M], 2 = B given as [N][K], 4 = an
+// f32 product through the six-piece bf16 split (bk_gemm_f32x6): the payload
+// then ends with a u64 workspace handle of f32x6_workspace_bytes(M, N, K)
+constexpr uint32_t kGemmFpSplit = 4;
 constexpr uint64_t kMaxFrame = 1ull << 30;         // largest request / READ reply
 constexpr int64_t kMaxLazyDraw = 1ll << 36;        // rand_reduce: ~70 ms of GPU at most
 constexpr uint64_t kMaxClientHandle = 1ull << 62;  // ALLOC_AT ids are 1 .. 2^62-1
@@ -51,6 +55,13 @@ inline bool range_ok(uint64_t off, uint64_t n, uint64_t size) { return off <= si
 bool matrix_bytes(int64_t rows, int64_t cols, int64_t ld, uint64_t esize, uint64_t* out);
 // the allocator's rounding (what an allocation really costs in HBM)
 uint64_t charged_bytes(uint64_t nbytes);
+// the split f32 product's workspace: a 256-byte header, then A' [M][6 Kp] and
+// B' [N][6 Kp] in bf16 with Kp = K rounded up to 64 (csrc/kernels/gemm_fp.hip
+// bk_gemm_f32x6_workspace_bytes, ops/array.py f32x6_workspace_bytes)
+inline uint64_t f32x6_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  return 256 + 12 * (uint64_t)((K + 63) / 64 * 64) * (uint64_t)(M + N);
+}
 
 // The GPU side of a session.  Every launch is asynchronous on `stream`
 // unless documented otherwise; non-zero int returns are beekern status codes.
@@ -95,6 +106,12 @@ class Device {
   // trans_b -> B given as [N][K]; kBadArgument where the device has no such kernel
   virtual int gemm_fp(uint32_t dt, bool trans_a, bool trans_b, const void*, const void*, void*, int, int, int, int64_t,
                       int64_t, int64_t, void*) {
+    return kBadArgument;
+  }
+  // the same f32 product on the bf16 MFMA through the six-piece split; ws is
+  // a workspace of f32x6_workspace_bytes(M, N, K), every byte of it written
+  virtual int gemm_f32x6(bool, bool, const void*, const void*, void*, int, int, int, int64_t, int64_t, int64_t, void*,
+                         uint64_t, void*) {
     return kBadArgument;
   }
   virtual int transpose(int sdt, int ddt, const void* in, void* out, int rows, int cols, int ldi, int ldo, void* s) = 0;

@@ -143,6 +143,12 @@ class HostDevice final : public Device {
     for (int i = 0; i < M; ++i) touch_w((char*)C + (uint64_t)i * ldc * es, (uint64_t)N * es, 0);
     return 0;
   }
+  int gemm_f32x6(bool ta, bool tb, const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb,
+                 int64_t ldc, void* ws, uint64_t ws_bytes, void* s) override {
+    if (ws_bytes != f32x6_workspace_bytes(M, N, K)) return kBadArgument;
+    touch_w(ws, ws_bytes, 0);  // the device writes every workspace byte
+    return gemm_fp(0, ta, tb, A, B, C, M, N, K, lda, ldb, ldc, s);
+  }
   int transpose(int sdt, int ddt, const void* in, void* out, int rows, int cols, int ldi, int ldo, void*) override {
     const uint64_t si = dtype_size((uint32_t)sdt), so = dtype_size((uint32_t)ddt);
     for (int i = 0; i < rows; ++i) sum((const char*)in + (uint64_t)i * ldi * si, (uint64_t)cols * si);

@@ -136,7 +136,11 @@ struct Tile {
 template <typename T, bool TA, bool TB, bool VEC, int BN, int BK, int OCC, bool VF>
 __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restrict__ a, const T* __restrict__ b,
                                                                T* __restrict__ c, int M, int N, int K, int64_t lda,
-                                                               int64_t ldb, int64_t ldc) {
+                                                               int64_t ldb, int64_t ldc,
+                                                               const unsigned* __restrict__ gate) {
+  // gated launch (the split-bf16 f32 product's fallback, bk_gemm_f32x6):
+  // runs only when the split found operands it cannot represent
+  if (gate && *gate == 0) return;
   constexpr int PK = Cfg<T>::pitch_k(BK);
   // vector fragment reads with a permuted k order (f32, BK % 16 == 0; f64's
   // registers are too tight for the 2x fragment set); opt-in, BK_GEMM_FP_VEC=1
@@ -325,7 +329,7 @@ inline bool narrow_tiles(int M, int N, int occ) {
 // depth in elements) override the choice for A/B runs (tools/gemm_fp_bench.py).
 template <typename T, bool TA, bool TB>
 void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, bool vec,
-            hipStream_t stream) {
+            hipStream_t stream, const unsigned* gate = nullptr) {
   const char* ebn = getenv("BK_GEMM_FP_BN");
   const char* ebk = getenv("BK_GEMM_FP_BK");
   // f32: a 64-byte K tile (16 deep) halves the LDS a workgroup holds, so a
@@ -352,10 +356,10 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
     if (vf && std::is_same<T, float>::value && (O) < 4) /* (at four per CU the vector reads spill) */          \
       gemm_fp_kernel<T, TA, TB, V, W, D, O, std::is_same<T, float>::value && (O) < 4><<<grid, kThreads, 0,       \
                                                                                      stream>>>(                \
-          (const T*)A, (const T*)B, (T*)C, M, N, K, lda, ldb, ldc);                                             \
+          (const T*)A, (const T*)B, (T*)C, M, N, K, lda, ldb, ldc, gate);                                             \
     else                                                                                                      \
       gemm_fp_kernel<T, TA, TB, V, W, D, O, false><<<grid, kThreads, 0, stream>>>((const T*)A, (const T*)B,     \
-                                                                                 (T*)C, M, N, K, lda, ldb, ldc); \
+                                                                                 (T*)C, M, N, K, lda, ldb, ldc, gate); \
   } while (0)
 #define BK_FP_DEPTH(D, O)          \
   do {                             \
@@ -385,15 +389,136 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
 
 template <typename T>
 void dispatch(bool ta, bool tb, const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb,
-              int64_t ldc, bool vec, hipStream_t s) {
+              int64_t ldc, bool vec, hipStream_t s, const unsigned* gate = nullptr) {
   if (ta && tb)
-    launch<T, true, true>(A, B, C, M, N, K, lda, ldb, ldc, vec, s);
+    launch<T, true, true>(A, B, C, M, N, K, lda, ldb, ldc, vec, s, gate);
   else if (ta)
-    launch<T, true, false>(A, B, C, M, N, K, lda, ldb, ldc, vec, s);
+    launch<T, true, false>(A, B, C, M, N, K, lda, ldb, ldc, vec, s, gate);
   else if (tb)
-    launch<T, false, true>(A, B, C, M, N, K, lda, ldb, ldc, vec, s);
+    launch<T, false, true>(A, B, C, M, N, K, lda, ldb, ldc, vec, s, gate);
   else
-    launch<T, false, false>(A, B, C, M, N, K, lda, ldb, ldc, vec, s);
+    launch<T, false, false>(A, B, C, M, N, K, lda, ldb, ldc, vec, s, gate);
+}
+
+
+// ---- f32 product on the bf16 MFMA: the six-piece split (bk_gemm_f32x6) ----
+//
+// An f32 value a (24-bit significand) is the exact sum of three bf16 pieces
+// (8 bits each): a0 = bf16(a), a1 = bf16(a - a0), a2 = bf16(a - a0 - a1); each
+// difference is exact (Sterbenz), so |a - (a0 + a1 + a2)| <= 2^-25 |a|.  A
+// product of two pieces has at most 16 significant bits, exact in the bf16
+// MFMA's f32 accumulator, and
+//   a . b = a0 b0 + a0 b1 + a1 b0 + a0 b2 + a1 b1 + a2 b0 + (a1 b2 + a2 b1 + a2 b2)
+// where the bracket is below 2^-24 |a b| -- f32's own rounding unit -- and is
+// dropped.  So one bf16 GEMM over K' = 6 Kp with
+//   A' row = [a0 | a0 | a1 | a0 | a1 | a2],  B' row = [b0 | b1 | b0 | b2 | b1 | b0]
+// (each block Kp = K rounded up to 64, zero-padded) gives the f32 product with
+// f32-level error (6x the additions of a plain f32 dot product), at the bf16
+// MFMA's rate: 6 x 2 x 2.5 PFLOP/s-class passes against f32's 157 TFLOP/s.
+//
+// The split needs |a| in [2^-100, 2^127) or a == 0: infinities and NaNs
+// (inf * a zero piece is NaN), values whose bf16 head overflows, and values
+// whose pieces fall below the normal range.  A piece kernel that meets one
+// sets the workspace's flag word (cleared first, on the stream); the plain f32
+// kernel is then launched gated on that flag and recomputes C only if set.
+constexpr uint32_t kSplitPatA = 0 | 0 << 2 | 1 << 4 | 0 << 6 | 1 << 8 | 2 << 10;
+constexpr uint32_t kSplitPatB = 0 | 1 << 2 | 0 << 4 | 2 << 6 | 1 << 8 | 0 << 10;
+constexpr int kSplitTile = 64;
+
+__device__ __forceinline__ uint32_t bf16_rn_bits(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// three pieces of 8 values, packed 8 bf16 per u32x4; true if any value is
+// outside the split's range
+__device__ __forceinline__ bool split8(const float (&x)[8], u32x4_t (&p)[3]) {
+  bool bad = false;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    uint32_t w[3] = {0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float a = x[2 * h + e];
+      const float m = fabsf(a);
+      bad |= !(m < 0x1p127f) || (m != 0.f && m < 0x1p-100f);
+      const uint32_t h0 = bf16_rn_bits(a);
+      const float r1 = a - __uint_as_float(h0 << 16);
+      const uint32_t h1 = bf16_rn_bits(r1);
+      const uint32_t h2 = bf16_rn_bits(r1 - __uint_as_float(h1 << 16));
+      w[0] |= h0 << (16 * e);
+      w[1] |= h1 << (16 * e);
+      w[2] |= h2 << (16 * e);
+    }
+    p[0][h] = w[0];
+    p[1][h] = w[1];
+    p[2][h] = w[2];
+  }
+  return bad;
+}
+
+// dst[r][j * Kp + k] = piece pat_j of src(r, k) for r < rows, k < Kp (zero past
+// K).  COLS: src(r, k) = src[k * ld + r] (an [K][rows] buffer, staged through
+// LDS to transpose), else src[r * ld + k].  One 64 x 64 tile per workgroup;
+// thread t handles rows t / 8 + 32 q (q = 0, 1) and the 8 k of chunk t % 8,
+// so each group of 8 lanes writes 128 contiguous bytes of each block.
+template <bool COLS, bool VEC>
+__global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ src, int rows, int K, int64_t ld, int Kp,
+                                                     uint16_t* __restrict__ dst, uint32_t pat,
+                                                     unsigned* __restrict__ flag) {
+  constexpr int T = kSplitTile, kPitch = T + 1;  // +1: the column reads below hit 64 banks
+  __shared__ float tile[COLS ? T * kPitch : 1];
+  const int tiles_k = Kp / T;
+  const int r0 = (int)(blockIdx.x / tiles_k) * T, k0 = (int)(blockIdx.x % tiles_k) * T;
+  const int tid = (int)threadIdx.x, kc = tid & 7;
+  const int64_t ldd = 6 * (int64_t)Kp;
+  if constexpr (COLS) {
+    // 64 k-lines of 64 rows: lane runs of 16 x 4 consecutive rows per line
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kl = (tid >> 4) + 16 * i, rr = (tid & 15) * 4;
+      const int k = k0 + kl, r = r0 + rr;
+      float v[4];
+      if (VEC && k < K && r + 4 <= rows) {
+        const f32x4 w = *reinterpret_cast<const f32x4*>(src + (int64_t)k * ld + r);
+        v[0] = w[0], v[1] = w[1], v[2] = w[2], v[3] = w[3];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (k < K && r + e < rows) ? src[(int64_t)k * ld + r + e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tile[kl * kPitch + rr + e] = v[e];
+    }
+    __syncthreads();
+  }
+  bool bad = false;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int rl = (tid >> 3) + 32 * q, r = r0 + rl, k = k0 + kc * 8;
+    if (r >= rows) continue;
+    float x[8];
+    if constexpr (COLS) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = tile[(kc * 8 + e) * kPitch + rl];
+    } else {
+      const float* p = src + (int64_t)r * ld + k;
+      if (VEC && k + 8 <= K) {
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(p), w1 = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = w0[e], x[4 + e] = w1[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = k + e < K ? p[e] : 0.f;
+      }
+    }
+    u32x4_t pc[3];
+    bad |= split8(x, pc);
+    uint16_t* o = dst + (int64_t)r * ldd + k;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) *reinterpret_cast<u32x4_t*>(o + (int64_t)j * Kp) = pc[(pat >> (2 * j)) & 3];
+  }
+  // (rare: a vector atomic from the lanes that found one)
+  if (bad) atomicOr(flag, 1u);
 }
 
 }  // namespace fp
@@ -419,5 +544,61 @@ BK_API int bk_gemm_fp(int dtype, int trans_a, int trans_b, const void* A, const 
     fp::dispatch<double>(trans_a != 0, trans_b != 0, A, B, C, M, N, K, lda, ldb, ldc, vec, stream);
   else
     fp::dispatch<float>(trans_a != 0, trans_b != 0, A, B, C, M, N, K, lda, ldb, ldc, vec, stream);
+  return launch_status();
+}
+
+
+// ---- C = op(A) . op(B) for f32 operands on the bf16 MFMA GEMM, f32-level
+// error (the six-piece split above).  Same operand conventions as
+// bk_gemm_fp.  `ws` (16-B aligned, bk_gemm_f32x6_workspace_bytes) holds a
+// flag word and the split operands A' [M][6 Kp], B' [N][6 Kp].  Operands the
+// split cannot represent (inf / NaN, |x| >= 2^127, 0 < |x| < 2^-100) make the
+// plain f32 kernel recompute C, gated on the flag (no host sync).
+BK_API int bk_gemm_bf16_tn(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                           float alpha, float beta, int out_dtype, hipStream_t stream);
+
+static int64_t f32x6_kp(int K) { return ((int64_t)K + fp::kSplitTile - 1) / fp::kSplitTile * fp::kSplitTile; }
+
+BK_API int64_t bk_gemm_f32x6_workspace_bytes(int M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  return 256 + 12 * f32x6_kp(K) * ((int64_t)M + N);
+}
+
+BK_API int bk_gemm_f32x6(int trans_a, int trans_b, const void* A, const void* B, void* C, int M, int N, int K,
+                         int64_t lda, int64_t ldb, int64_t ldc, void* ws, int64_t ws_bytes, hipStream_t stream) {
+  if (!A || !B || !C || !ws || M <= 0 || N <= 0 || K <= 0) return kBadArgument;
+  if (lda < (trans_a ? M : K) || ldb < (trans_b ? K : N) || ldc < N || ldc > 0x7fffffffll) return kBadArgument;
+  const int64_t kp = f32x6_kp(K);
+  // the bf16 kernels' int K / leading dimensions and 31-bit tile extents
+  if (6 * kp > (1 << 22) || ws_bytes < bk_gemm_f32x6_workspace_bytes(M, N, K) || (uintptr_t)ws % 16) return kBadArgument;
+  unsigned* flag = (unsigned*)ws;
+  // the header (flag word + padding) is written, so every workspace byte is
+  // (the broker's lazy scrub counts on that for an exactly-sized workspace)
+  if (hipMemsetAsync(ws, 0, 256, stream) != hipSuccess) return kLaunchFailed;
+  uint16_t* a6 = (uint16_t*)((char*)ws + 256);
+  uint16_t* b6 = a6 + 6 * kp * (int64_t)M;
+  auto split = [&](bool cols, const void* src, int rows, int64_t ld, uint16_t* dst, uint32_t pat) {
+    const bool vec = (uintptr_t)src % 16 == 0 && ld % 4 == 0;
+    const unsigned grid = (unsigned)(((rows + fp::kSplitTile - 1) / fp::kSplitTile) * (kp / fp::kSplitTile));
+    const float* s = (const float*)src;
+    if (cols && vec)
+      fp::split3_kernel<true, true><<<grid, 256, 0, stream>>>(s, rows, K, ld, (int)kp, dst, pat, flag);
+    else if (cols)
+      fp::split3_kernel<true, false><<<grid, 256, 0, stream>>>(s, rows, K, ld, (int)kp, dst, pat, flag);
+    else if (vec)
+      fp::split3_kernel<false, true><<<grid, 256, 0, stream>>>(s, rows, K, ld, (int)kp, dst, pat, flag);
+    else
+      fp::split3_kernel<false, false><<<grid, 256, 0, stream>>>(s, rows, K, ld, (int)kp, dst, pat, flag);
+  };
+  // A(m, k): [M][K] rows, or the [K][M] buffer of an A^T view (columns);
+  // B(n, k): the [N][K] buffer of a B^T view (rows), or [K][N] (columns)
+  split(trans_a != 0, A, M, lda, a6, fp::kSplitPatA);
+  split(trans_b == 0, B, N, ldb, b6, fp::kSplitPatB);
+  int rc = launch_status();
+  if (rc != kOk) return rc;
+  rc = bk_gemm_bf16_tn(a6, b6, C, M, N, (int)(6 * kp), (int)(6 * kp), (int)(6 * kp), (int)ldc, 1.f, 0.f, kF32, stream);
+  if (rc != kOk) return rc;
+  const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % 4 == 0 && ldb % 4 == 0;
+  fp::dispatch<float>(trans_a != 0, trans_b != 0, A, B, C, M, N, K, lda, ldb, ldc, vec, stream, flag);
   return launch_status();
 }

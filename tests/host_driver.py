@@ -197,6 +197,13 @@ class HostDriver:
         c[:, :N] = prod
         self._store(C, c.ravel(), dt)
 
+    def gemm_f32x6(self, ta, tb, A, B, C, M, N, K, lda, ldb, ldc, W, ws_bytes) -> None:
+        self.launches.append(("gemm_f32x6", M, N, K, bool(ta), bool(tb)))
+        assert ws_bytes == 256 + 12 * ((K + 63) // 64 * 64) * (M + N)
+        self._load(W, ws_bytes // 2, 2)  # (the workspace exists and is that large)
+        self.gemm_fp(0, ta, tb, A, B, C, M, N, K, lda, ldb, ldc)
+        self.launches.pop()  # (the inner gemm_fp's own entry)
+
     def _gemm_out(self, prod, C, M, N, ldc, alpha, beta, odt):
         c = self._load(C, M * ldc, odt).reshape(M, ldc)
         c[:, :N] = alpha * prod.astype(np.float32) + (beta * c[:, :N] if beta else 0.0)

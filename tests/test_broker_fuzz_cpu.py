@@ -194,9 +194,12 @@ def _random_frames(seed: int, n: int):
             payload = struct.pack("<QQQiiiiiiffii", h(), h(), h(), i32(), i32(), i32(), i32(), i32(), i32(), 1.0,
                                   rnd.choice([0.0, 1.0]), rnd.choice([0, 2, 1, -1]), rnd.choice([0, 1, 2]))
         elif op == GEMM_FP:
-            payload = struct.pack("<IIQQQiiiiqqq", rnd.choice([0, 1, 2, 99]), rnd.choice([0, 1, 2, 3, 4]), h(), h(), h(),
+            gflags = rnd.choice([0, 1, 2, 3, 4, 5, 6, 7, 8])
+            payload = struct.pack("<IIQQQiiiiqqq", rnd.choice([0, 1, 2, 99]), gflags, h(), h(), h(),
                                   i32(), i32(), i32(), 0, num() % 5000 if rnd.random() < 0.5 else num() >> 1,
                                   num() % 5000, num() % 5000)
+            if gflags & 4 and rnd.random() < 0.8:  # the split's workspace handle
+                payload += struct.pack("<Q", h())
         elif op == TRANSPOSE:
             payload = struct.pack("<QQiiiiII", h(), h(), i32(), i32(), i32(), i32(), small(), small())
         elif op == FILL:
@@ -360,8 +363,43 @@ def test_refused_op_leaves_output_scrubbed(fuzz_bin):
     assert st[10] == BAD_ARG and st[11] == OK and rows[11][4] == bytes(64), rows[10:]
 
 
-def _gemm_fp(dt, flags, A, B, C, M, N, K, lda, ldb, ldc):
-    return frame(GEMM_FP, struct.pack("<IIQQQiiiiqqq", dt, flags, A, B, C, M, N, K, 0, lda, ldb, ldc))
+def _gemm_fp(dt, flags, A, B, C, M, N, K, lda, ldb, ldc, ws=None):
+    tail = b"" if ws is None else struct.pack("<Q", ws)
+    return frame(GEMM_FP, struct.pack("<IIQQQiiiiqqq", dt, flags, A, B, C, M, N, K, 0, lda, ldb, ldc) + tail)
+
+
+def _f32x6_ws(M, N, K):  # broker_core.hpp f32x6_workspace_bytes
+    return 256 + 12 * ((K + 63) // 64 * 64) * (M + N)
+
+
+def test_gemm_fp_split_workspace_is_bounded_and_exclusive(fuzz_bin):
+    """GEMM_FP flag 4 (the f32 product through the six-piece bf16 split,
+    ops/array.py matmul_fp): the trailing workspace handle must name a buffer
+    of at least f32x6_workspace_bytes(M, N, K) that is none of the operands;
+    f32 only; without the handle the frame is truncated."""
+    A, B, C, W, W2 = 1 << 62, (1 << 62) + 1, (1 << 62) + 2, (1 << 62) + 3, (1 << 62) + 4
+    M, N, K = 64, 32, 16
+    need = _f32x6_ws(M, N, K)
+    frames = [
+        frame(ALLOC, struct.pack("<Q", M * K * 4)),
+        frame(ALLOC, struct.pack("<Q", K * N * 4)),
+        frame(ALLOC, struct.pack("<Q", M * N * 4)),
+        frame(ALLOC, struct.pack("<Q", need)),
+        frame(ALLOC, struct.pack("<Q", need - 1)),
+        _gemm_fp(0, 4, A, B, C, M, N, K, K, N, N, W),        # 5: exact workspace: ok
+        _gemm_fp(0, 4, A, B, C, M, N, K, K, N, N, W2),       # 6: one byte short
+        _gemm_fp(1, 4, A, B, C, M, N, K, K, N, N, W),        # 7: f64 has no split
+        _gemm_fp(0, 4, A, B, C, M, N, K, K, N, N, C),        # 8: workspace = the output
+        _gemm_fp(0, 4, A, B, C, M, N, K, K, N, N),           # 9: handle missing
+        _gemm_fp(0, 7, A, B, C, M, N, K // 2, M, K // 2, N, W),  # 10: both views, half K: fits
+        _gemm_fp(0, 4, A, B, C, M, N, K, K, N, N, 12345),    # 11: no such workspace
+        frame(READ, struct.pack("<QQQ", W, 0, 64)),          # 12: the workspace was written, not scrubbed
+    ]
+    rows = run(fuzz_bin, frames)
+    st = [r[1] for r in rows]
+    assert st[:6] == [OK] * 6, st
+    assert st[6:9] == [BAD_HANDLE] * 3 and st[9] == PROTOCOL, st
+    assert st[10] == OK and st[11] == BAD_HANDLE and st[12] == OK, st
 
 
 def test_gemm_fp_extents_follow_the_transpose_flags(fuzz_bin):
@@ -381,7 +419,7 @@ def test_gemm_fp_extents_follow_the_transpose_flags(fuzz_bin):
         _gemm_fp(1, 1, A, B, C, M, N, K, M + 1, N, N),             # 6: lda past A
         _gemm_fp(1, 2, A, B, C, M, N, K, K, K + 200, N),           # 7: ldb past B
         _gemm_fp(1, 0, A, B, C, M, N, K, K, N, 2**62),             # 8: ldc * M wraps
-        _gemm_fp(1, 4, A, B, C, M, N, K, K, N, N),                 # 9: unknown flag
+        _gemm_fp(1, 8, A, B, C, M, N, K, K, N, N),                 # 9: unknown flag
         _gemm_fp(2, 0, A, B, C, M, N, K, K, N, N),                 # 10: bf16 is not this op's
         _gemm_fp(0, 0, A, B, C, 2 * M, 2 * N, K, K, 2 * N, 2 * N),  # 11: f32 2Mx2N > C
         _gemm_fp(0, 3, A, B, C, M, N, 2 * K, M, 2 * K, N),         # 12: f32, both views: fits (half the bytes)

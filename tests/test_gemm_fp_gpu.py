@@ -5,7 +5,9 @@ from the fp64 reference only by the rounding of a blocked dot product
 (relative error <= 1e-12 * sqrt(K) of the magnitude scale |A|.|B|), an f32
 product by f32 rounding (<= 1e-5).  Every transpose combination is a
 ``.T`` view read in place; ragged shapes, unaligned leading dimensions,
-vectors and NaNs are covered."""
+vectors and NaNs are covered.  Large f32 products run on the bf16 MFMA
+through the six-piece split (``bk_gemm_f32x6``) under the same f32 bound;
+operands the split cannot represent take the plain f32 kernel, bitwise."""
 
 import math
 
@@ -106,3 +108,68 @@ def test_unmodified_numpy_matmul_under_offload(gpu, monkeypatch):
     a_h, b_h, g_h = np.asarray(a), np.asarray(b), np.asarray(g)
     _check(np.asarray(c), a_h, b_h, "float64")
     _check(np.asarray(d), g_h.T, g_h, "float64")
+
+
+def _x6(gpu, a_h, b_h, ta, tb, M, N, K):
+    """bk_gemm_f32x6 through the driver; a_h / b_h are the stored buffers."""
+    from bee_code_interpreter_fs_amd.ops.array import DeviceArray, driver, f32x6_workspace_bytes
+
+    a, b = gpu.asarray(a_h), gpu.asarray(b_h)
+    c = DeviceArray((M, N), "float32")
+    nbytes = f32x6_workspace_bytes(M, N, K)
+    ws = DeviceArray((nbytes // 2,), "bfloat16")
+    driver().gemm_f32x6(ta, tb, a.ptr, b.ptr, c.ptr, M, N, K, a_h.shape[1], b_h.shape[1], N, ws.ptr, nbytes)
+    return c.numpy()
+
+
+def _native_f32(gpu, a_h, b_h, ta, tb, M, N, K):
+    from bee_code_interpreter_fs_amd.ops.array import DeviceArray, driver
+
+    a, b = gpu.asarray(a_h), gpu.asarray(b_h)
+    c = DeviceArray((M, N), "float32")
+    driver().gemm_fp(0, ta, tb, a.ptr, b.ptr, c.ptr, M, N, K, a_h.shape[1], b_h.shape[1], N)
+    return c.numpy()
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 200, 260), (1000, 777, 333), (129, 1030, 17)])
+def test_gemm_f32x6_matches_fp64(gpu, M, N, K, ta, tb):
+    """The split product: f32-level error in every orientation, ragged M, N
+    and K (the pieces' K blocks are zero-padded to 64)."""
+    rng = np.random.default_rng(M + 5 * N + 11 * K + 2 * ta + tb)
+    a_h = rng.standard_normal((K, M) if ta else (M, K)).astype(np.float32)
+    b_h = rng.standard_normal((N, K) if tb else (K, N)).astype(np.float32)
+    c = _x6(gpu, a_h, b_h, ta, tb, M, N, K)
+    a64, b64 = a_h.astype(np.float64), b_h.astype(np.float64)
+    _check(c, a64.T if ta else a64, b64.T if tb else b64, "float32")
+
+
+@pytest.mark.parametrize("bad", [np.inf, -np.inf, np.nan, 3.0e38, 1.0e-35, -2.0e-33])
+def test_gemm_f32x6_falls_back_bitwise_outside_the_split_range(gpu, bad):
+    """inf / NaN (inf times a zero piece would be NaN), values whose bf16 head
+    overflows and values whose pieces leave the normal range: the gated f32
+    kernel recomputes C, so the result is the plain f32 kernel's, bitwise."""
+    M, N, K = 256, 320, 96
+    rng = np.random.default_rng(9)
+    a_h = rng.standard_normal((M, K)).astype(np.float32)
+    b_h = rng.standard_normal((K, N)).astype(np.float32)
+    b_h[17, 33] = bad
+    got = _x6(gpu, a_h, b_h, False, False, M, N, K)
+    want = _native_f32(gpu, a_h, b_h, False, False, M, N, K)
+    np.testing.assert_array_equal(got, want)
+    # and back in range, the split runs again (the flag is per call)
+    b_h[17, 33] = 0.5
+    c = _x6(gpu, a_h, b_h, False, False, M, N, K)
+    _check(c, a_h.astype(np.float64), b_h.astype(np.float64), "float32")
+
+
+def test_large_f32_matmul_routes_to_the_split_and_keeps_f32_precision(gpu):
+    """gpu.matmul of a 2048 x 2048 x 1024 f32 product (2^32 multiply-adds)
+    takes the split; the error against fp64 stays at f32 rounding level."""
+    rng = np.random.default_rng(21)
+    a_h = rng.uniform(-1, 1, (2048, 1024)).astype(np.float32)
+    b_h = rng.uniform(-1, 1, (1024, 2048)).astype(np.float32)
+    c = gpu.matmul(gpu.asarray(a_h), gpu.asarray(b_h)).numpy()
+    a64, b64 = a_h.astype(np.float64), b_h.astype(np.float64)
+    err = np.abs(c - a64 @ b64) / (np.abs(a64) @ np.abs(b64))
+    assert float(err.max()) < 2e-6, float(err.max())

@@ -138,6 +138,26 @@ def test_broker_matmul_wide_operands(gsvc):
     assert r.stdout.split() == ["True", "True", "rejected"], (r.stdout, r.stderr)
 
 
+def test_broker_f32_matmul_through_the_split(gsvc):
+    """Through the broker: a large f32 product takes the six-piece bf16 split
+    (GEMM_FP flag 4 with its workspace handle) at f32 precision, and an inf
+    operand takes the gated f32 kernel (numpy's inf, no NaN from the split)."""
+    code = (
+        "import numpy as np, beekern as bk\n"
+        "rng = np.random.default_rng(4)\n"
+        "a = rng.uniform(-1, 1, (2048, 1024)).astype(np.float32); b = rng.uniform(-1, 1, (1024, 2048)).astype(np.float32)\n"
+        "c = bk.matmul(bk.asarray(a), bk.asarray(b)).numpy()\n"
+        "ref = a.astype(np.float64) @ b.astype(np.float64)\n"
+        "sc = np.abs(a.astype(np.float64)) @ np.abs(b.astype(np.float64))\n"
+        "print(float((np.abs(c - ref) / sc).max()) < 2e-6)\n"
+        "b[3, 5] = np.inf\n"
+        "c = bk.matmul(bk.asarray(np.abs(a)), bk.asarray(b)).numpy()\n"
+        "print(bool(np.isinf(c[:, 5]).all()), bool(np.isfinite(np.delete(c, 5, axis=1)).all()))\n"
+    )
+    r = run(gsvc, code)
+    assert r.stdout.split() == ["True", "True", "True"], (r.stdout, r.stderr)
+
+
 def test_torch_inside_sandbox(gsvc):
     code = (
         "import torch\n"

@@ -33,6 +33,17 @@ def gemm(lib, a, b, c, ta=False, tb=False):
         raise RuntimeError(f"bk_gemm_fp rc={rc}")
 
 
+def gemm_x6(lib, a, b, c, ws, ta=False, tb=False):
+    """f32 on the bf16 MFMA via the six-piece split (bk_gemm_f32x6)."""
+    M = a.shape[1] if ta else a.shape[0]
+    K = a.shape[0] if ta else a.shape[1]
+    N = b.shape[0] if tb else b.shape[1]
+    rc = lib.bk_gemm_f32x6(int(ta), int(tb), a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, a.shape[1],
+                           b.shape[1], c.shape[1], ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"bk_gemm_f32x6 rc={rc}")
+
+
 def timeit(fn, rounds, reps):
     out = []
     for _ in range(rounds):
@@ -46,7 +57,7 @@ def timeit(fn, rounds, reps):
     return out
 
 
-def bench(lib, dtype, M, N, K, rounds, reps, ta=False, tb=False):
+def bench(lib, dtype, M, N, K, rounds, reps, ta=False, tb=False, x6=False):
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + 7 * K)
     a = torch.empty((K, M) if ta else (M, K), device="cuda", dtype=dtype).uniform_(-1, 1, generator=g)
     b = torch.empty((N, K) if tb else (K, N), device="cuda", dtype=dtype).uniform_(-1, 1, generator=g)
@@ -68,6 +79,15 @@ def bench(lib, dtype, M, N, K, rounds, reps, ta=False, tb=False):
         gemm(lib, a, b, c, ta, tb)
         racy += int(not torch.equal(c, first))
     fns = {"beekern": lambda: gemm(lib, a, b, c, ta, tb), "torch": lambda: torch.matmul(aa, bb, out=ct)}
+    extra = {}
+    if x6 and dtype == torch.float32:
+        ws = torch.empty(lib.bk_gemm_f32x6_workspace_bytes(M, N, K), device="cuda", dtype=torch.uint8)
+        cx = torch.empty(M, N, device="cuda", dtype=dtype)
+        gemm_x6(lib, a, b, cx, ws, ta, tb)
+        torch.cuda.synchronize()
+        extra["max_rel_err_x6"] = ((cx.double() - ref).abs() / scale).max().item()
+        extra["max_abs_rel_to_native_x6"] = ((cx.double() - c.double()).abs() / scale).max().item()
+        fns["x6"] = lambda: gemm_x6(lib, a, b, cx, ws, ta, tb)
     for f in fns.values():
         f()
     times = {k: [] for k in fns}
@@ -76,12 +96,14 @@ def bench(lib, dtype, M, N, K, rounds, reps, ta=False, tb=False):
             times[name] += timeit(f, 1, reps)
     flops = 2.0 * M * N * K
     r = {"dtype": str(dtype).replace("torch.", ""), "shape": f"{M}x{N}x{K}", "ta": ta, "tb": tb,
-         "max_rel_err_beekern": err_bk, "max_rel_err_torch": err_t, "racy_repeats": racy}
+         "max_rel_err_beekern": err_bk, "max_rel_err_torch": err_t, "racy_repeats": racy, **extra}
     for name, t in times.items():
         r[f"{name}_us_median"] = round(1e3 * statistics.median(t), 1)
         r[f"{name}_tflops_median"] = round(flops / statistics.median(t) / 1e9, 1)
         r[f"{name}_tflops_best"] = round(flops / min(t) / 1e9, 1)
     r["ratio_median"] = round(statistics.median(times["torch"]) / statistics.median(times["beekern"]), 3)
+    if "x6" in times:
+        r["ratio_median_x6"] = round(statistics.median(times["torch"]) / statistics.median(times["x6"]), 3)
     return r
 
 
@@ -92,18 +114,19 @@ def main():
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--reps", type=int, default=10)
     p.add_argument("--transposes", action="store_true", help="also A^T and B^T views at the first size")
+    p.add_argument("--x6", action="store_true", help="f32: also the six-piece bf16 split (bk_gemm_f32x6)")
     args = p.parse_args()
     torch.cuda.init()
     lib = _native.lib()
     for dt in args.dtypes:
         dtype = getattr(torch, dt)
         for n in args.sizes:
-            print(json.dumps(bench(lib, dtype, n, n, n, args.rounds, args.reps)), flush=True)
+            print(json.dumps(bench(lib, dtype, n, n, n, args.rounds, args.reps, x6=args.x6)), flush=True)
         if args.transposes:
             n = args.sizes[0]
             for ta, tb in ((True, False), (False, True)):
-                print(json.dumps(bench(lib, dtype, n, n, n, args.rounds, args.reps, ta, tb)), flush=True)
-        print(json.dumps(bench(lib, dtype, 4000, 3000, 1000, args.rounds, args.reps)), flush=True)
+                print(json.dumps(bench(lib, dtype, n, n, n, args.rounds, args.reps, ta, tb, x6=args.x6)), flush=True)
+        print(json.dumps(bench(lib, dtype, 4000, 3000, 1000, args.rounds, args.reps, x6=args.x6)), flush=True)
 
 
 if __name__ == "__main__":
