@@ -220,7 +220,10 @@ void stress() {
         while (now > p && !peak.compare_exchange_weak(p, now)) {
         }
         if ((hbm += c.hbm) > (64 << 20)) over = true;
-        std::this_thread::yield();
+        // hold the job a moment: with a bare yield, a loaded CPU (the suite
+        // under TSan) could run the threads one after another and never
+        // overlap two jobs
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
         hbm -= c.hbm;
         --running;
         a.finish(c);
