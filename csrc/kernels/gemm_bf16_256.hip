@@ -6,6 +6,8 @@
 // (profiles/archive/r1_gemm_lab.log): the 4-wave kernel issues half the LDS reads per
 // MFMA and wins from K >= 256 on (4096^3: 1401 vs 1259 TFLOP/s); the 8-wave
 // kernel wins short-K shapes, where the 4-wave prologue/epilogue dominate.
+#include <cstring>
+
 #include "gemm256_impl.hpp"
 #include "gemm256w4_impl.hpp"
 
@@ -27,10 +29,23 @@ bool gemm256_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16) {
   return g256::ok(M, N, K, lda, ldb, ldc, out_bf16);
 }
 
+// BK_GEMM256=w8 | w4: the kernel `which == 0` resolves to for every shape
+// (A/B runs of the served path: the 8-wave kernel's 214 VGPRs leave room on
+// each SIMD for another sandbox's VALU-bound waves, the 4-wave kernel's 512
+// do not)
+static int forced_which() {
+  static const int w = [] {
+    const char* e = getenv("BK_GEMM256");
+    return !e ? 0 : !strcmp(e, "w8") ? 1 : !strcmp(e, "w4") ? 2 : 0;
+  }();
+  return w;
+}
+
 // which: 0 = by shape, 1 = 8-wave, 2 = 4-wave
 void launch_gemm256(const void* A, const void* Bt, void* C, int M, int N, int K, int lda, int ldb, int ldc, float alpha,
                     float beta, bool out_bf16, hipStream_t stream, int which) {
   const bool w4_ok = g4::ok(M, N, K, lda, ldb, ldc, out_bf16);
+  if (which == 0) which = forced_which();
   if (which == 0) which = (w4_ok && K >= kW4MinK) ? 2 : 1;
   if (which == 2 && w4_ok)
     g4::launch<kShippedW4>(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, out_bf16, stream);
