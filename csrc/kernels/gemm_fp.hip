@@ -137,7 +137,10 @@ template <typename T, bool TA, bool TB, bool VEC, int BN, int BK, int OCC, bool 
 __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restrict__ a, const T* __restrict__ b,
                                                                T* __restrict__ c, int M, int N, int K, int64_t lda,
                                                                int64_t ldb, int64_t ldc,
-                                                               const unsigned* __restrict__ gate) {
+                                                               const unsigned* __restrict__ gate, int splits_arg) {
+  // (the opt-in four-per-CU build has no register to spare for the atomic
+  // epilogue: no split-K there)
+  const int splits = OCC >= 4 ? 1 : splits_arg;
   // gated launch (the split-bf16 f32 product's fallback, bk_gemm_f32x6):
   // runs only when the split found operands it cannot represent
   if (gate && *gate == 0) return;
@@ -157,6 +160,12 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
   const int tiles_m = (M + kBM - 1) / kBM, tiles_n = (N + BN - 1) / BN;
   const int total = tiles_m * tiles_n;
   int bid = (int)blockIdx.x;
+  // split-K (splits == 2, small grids): blocks [total, 2 total) take the
+  // second half of the K tiles and both halves add into a zeroed C -- two
+  // atomic adds onto 0 give fl(p0 + p1) in either order, so the result is
+  // deterministic (three or more would not be)
+  const int half = splits > 1 && bid >= total ? 1 : 0;
+  bid -= half * total;
   if (total % kNumXCD == 0) bid = (bid % kNumXCD) * (total / kNumXCD) + bid / kNumXCD;
   constexpr int kGroup = 8;
   const int per_group = kGroup * tiles_n;
@@ -210,11 +219,13 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
   // (The one-ahead loop this replaced waited for its loads right before the
   // barrier: rocprofv3 SQ_WAIT_ANY 18% of f32 wave cycles against
   // torch.matmul's 3%, profiles/r5_gemm_fp_pmc.md.)
-  const int nk = (K + BK - 1) / BK;
-  load(0);
+  const int nk_all = (K + BK - 1) / BK, nk_first = splits > 1 ? (nk_all + 1) / 2 : nk_all;
+  const int kt0 = half ? nk_first : 0;  // this block's K tiles: [kt0, kt0 + nk)
+  const int nk = half ? nk_all - nk_first : nk_first;
+  load(kt0 * BK);
   ta.store(lds_a[0]);
   tb.store(lds_b[0]);
-  if (nk > 1) load(BK);
+  if (nk > 1) load((kt0 + 1) * BK);
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
@@ -222,7 +233,7 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
     if (kt + 1 < nk) {
       ta.store(lds_a[cur ^ 1]);
       tb.store(lds_b[cur ^ 1]);
-      if (kt + 2 < nk) load((kt + 2) * BK);
+      if (kt + 2 < nk) load((kt0 + kt + 2) * BK);
     }
     const T* As = lds_a[cur];
     const T* Bs = lds_b[cur];
@@ -296,7 +307,12 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int n = n0 + wn + j * 16 + fr;
-        if (n < N) crow[n] = acc[i][j][r];
+        if (n < N) {
+          if (splits > 1)
+            unsafeAtomicAdd(crow + n, (T)acc[i][j][r]);  // (hardware float add; C was zeroed)
+          else
+            crow[n] = acc[i][j][r];
+        }
       }
     }
   }
@@ -346,7 +362,23 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   const int occ = std::is_same<T, float>::value && bk == 16 ? (kOcc4 && eocc && atoi(eocc) == 4 ? 4 : 3) : 2;
   const bool nar = ebn ? atoi(ebn) == 64 : narrow_tiles(M, N, occ);
   const int bn = nar ? 64 : 128;
-  const unsigned grid = (unsigned)(((M + kBM - 1) / kBM) * ((N + bn - 1) / bn));
+  const int64_t tiles = (int64_t)((M + kBM - 1) / kBM) * ((N + bn - 1) / bn);
+  // split-K in two when the tiles fill at most half the chip's workgroup
+  // slots and each half keeps >= 8 K tiles (1024^3 f32: 128 tiles on 768
+  // slots); not for the gated fallback, whose C the split product wrote.
+  // BK_GEMM_FP_SPLITK=0 turns it off.
+  const char* esk = getenv("BK_GEMM_FP_SPLITK");
+  const int splits = !gate && occ < 4 && !(esk && atoi(esk) == 0) && 2 * tiles <= (int64_t)occ * kNumCU &&
+                             (K + bk - 1) / bk >= 16
+                         ? 2
+                         : 1;
+  if (splits > 1) {  // both halves add into C
+    const size_t row = (size_t)N * sizeof(T);
+    const hipError_t e = ldc == N ? hipMemsetAsync(C, 0, row * (size_t)M, stream)
+                                  : hipMemset2DAsync(C, (size_t)ldc * sizeof(T), 0, row, (size_t)M, stream);
+    if (e != hipSuccess) return;
+  }
+  const unsigned grid = (unsigned)(tiles * splits);
   // vector fragment reads (BK_GEMM_FP_VEC=1): measured no faster on MI355X
   // (4096^3 f32 126.7 vs 132.1 TFLOP/s, 8192^3 134.4 vs 135.0; their 5 more
   // VGPRs cost a wave per SIMD), so the plain reads are the default
@@ -356,10 +388,10 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
     if (vf && std::is_same<T, float>::value && (O) < 4) /* (at four per CU the vector reads spill) */          \
       gemm_fp_kernel<T, TA, TB, V, W, D, O, std::is_same<T, float>::value && (O) < 4><<<grid, kThreads, 0,       \
                                                                                      stream>>>(                \
-          (const T*)A, (const T*)B, (T*)C, M, N, K, lda, ldb, ldc, gate);                                             \
+          (const T*)A, (const T*)B, (T*)C, M, N, K, lda, ldb, ldc, gate, splits);                                             \
     else                                                                                                      \
       gemm_fp_kernel<T, TA, TB, V, W, D, O, false><<<grid, kThreads, 0, stream>>>((const T*)A, (const T*)B,     \
-                                                                                 (T*)C, M, N, K, lda, ldb, ldc, gate); \
+                                                                                 (T*)C, M, N, K, lda, ldb, ldc, gate, splits); \
   } while (0)
 #define BK_FP_DEPTH(D, O)          \
   do {                             \

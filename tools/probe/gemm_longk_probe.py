@@ -36,7 +36,7 @@ def main():
     lib = _native.lib()
     st = torch.cuda.current_stream().cuda_stream
     M = N = 4096
-    for K in (4096, 8192, 16384, 24576):
+    for K in [int(k) for k in os.environ.get("PROBE_KS", "4096 8192 16384 24576").split()]:
         a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         c = torch.empty(M, N, device="cuda", dtype=torch.float32)
@@ -51,7 +51,15 @@ def main():
         r = {"M": M, "N": N, "K": K, "bk_us": round(t(bk), 1),
              "torch_bf16_us": round(t(lambda: torch.matmul(a, b.T)), 1)}
         r["bk_pflops"] = round(2 * M * N * K / r["bk_us"] / 1e9, 3)
-        for ch in (2, 3, 6):
+        for v in (4, 5):  # the 256^2 kernel with 8 waves / 4 waves, forced
+
+            def var(v=v):
+                rc = lib.bk_gemm_bf16_tn_variant(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, K, K, N, 1.0, 0.0,
+                                                 0, v, st)
+                assert rc == 0, rc
+
+            r[f"bk_variant{v}_us"] = round(t(var), 1)
+        for ch in (2, 3, 6) if os.environ.get("PROBE_CHUNKS", "1") == "1" else ():
             if K % (ch * 64) == 0 and K // ch >= 4096:
                 r[f"bk_chunks{ch}_us"] = round(t(lambda ch=ch: bk(K, ch)), 1)
         print(json.dumps(r), flush=True)
