@@ -173,3 +173,30 @@ def test_large_f32_matmul_routes_to_the_split_and_keeps_f32_precision(gpu):
     a64, b64 = a_h.astype(np.float64), b_h.astype(np.float64)
     err = np.abs(c - a64 @ b64) / (np.abs(a64) @ np.abs(b64))
     assert float(err.max()) < 2e-6, float(err.max())
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+def test_gemm_fp_split_k_is_deterministic_and_keeps_c_gaps(gpu, dtype):
+    """Small products split K in two (both halves add into a zeroed C): the
+    result is bitwise the same on every repeat, within the dtype's bound, and
+    a C with ldc > N keeps the columns past N untouched."""
+    from bee_code_interpreter_fs_amd.ops import _native
+    from bee_code_interpreter_fs_amd.ops.array import DeviceArray, driver
+
+    M, N, K, ldc = 200, 136, 1024, 150
+    rng = np.random.default_rng(17)
+    A = rng.standard_normal((M, K)).astype(dtype)
+    B = rng.standard_normal((K, N)).astype(dtype)
+    a, b = gpu.asarray(A), gpu.asarray(B)
+    c = gpu.asarray(np.full((M, ldc), 7.0, dtype=dtype))
+    dt = _native.DTYPE_CODES[dtype]
+    driver().gemm_fp(dt, False, False, a.ptr, b.ptr, c.ptr, M, N, K, K, N, ldc)
+    first = c.numpy()
+    assert (first[:, N:] == 7.0).all()
+    _check(first[:, :N], A.astype(np.float64), B.astype(np.float64), dtype)
+    for _ in range(3):
+        driver().gemm_fp(dt, False, False, a.ptr, b.ptr, c.ptr, M, N, K, K, N, ldc)
+        np.testing.assert_array_equal(c.numpy(), first)
+    big = gpu.matmul(gpu.asarray(rng.standard_normal((1024, 1024)).astype(dtype)),
+                     gpu.asarray(rng.standard_normal((1024, 1024)).astype(dtype)))
+    assert isinstance(big, DeviceArray)
