@@ -32,6 +32,10 @@
 //    contiguous run of tiles, walked in groups of 8 tile rows (the A row
 //    panels and B column panels a group shares stay in that XCD's L2).
 //
+// Small products (fewer 128 x 64 tiles than half the chip's workgroup slots)
+// take 64 x 64 tiles and, while still at most half full, a deterministic
+// two-way split-K (profiles/r5_gemm_fp_bm64.jsonl, r5_gemm_fp_splitk.jsonl).
+//
 // Any M, N, K and leading dimensions: out-of-range elements load as zero and
 // stores are masked; 16-B loads where pointers and leading dimensions allow,
 // element loads otherwise.
@@ -133,7 +137,7 @@ struct Tile {
 // b[TB ? n*ldb + k : k*ldb + n].  Workgroup tile 128 x BN (BN = 128, or 64
 // when 128^2 tiles would leave CUs with a single workgroup); 4 waves of
 // 64 x BN/2.
-template <typename T, bool TA, bool TB, bool VEC, int BN, int BK, int OCC, bool VF>
+template <typename T, bool TA, bool TB, bool VEC, int BN, int BK, int OCC, bool VF, int BM = kBM>
 __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restrict__ a, const T* __restrict__ b,
                                                                T* __restrict__ c, int M, int N, int K, int64_t lda,
                                                                int64_t ldb, int64_t ldc,
@@ -145,19 +149,21 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
   // runs only when the split found operands it cannot represent
   if (gate && *gate == 0) return;
   constexpr int PK = Cfg<T>::pitch_k(BK);
+  // BM = 64 (small products): each wave 32 rows -- MI 16-row blocks
+  constexpr int MI = BM / 32, kPitchM = BM + 16;
   // vector fragment reads with a permuted k order (f32, BK % 16 == 0; f64's
   // registers are too tight for the 2x fragment set); opt-in, BK_GEMM_FP_VEC=1
   constexpr bool kVecFrag = std::is_same<T, float>::value && BK % 16 == 0 && VF;
   constexpr int kPitchN = BN + 16;  // a [k][n] row: f64 = 32, f32 = 16 dwords mod 64 banks
   constexpr int WN = BN / 2, NT = WN / 16;  // wave columns, 16-wide MFMA tiles per wave row
   // A tile: [m][k] (row-major A) or [k][m] (A^T view); B tile: [k][n] or [n][k]
-  using TileA = typename std::conditional<TA, Tile<T, VEC, BK, kBM, kPitchMN>, Tile<T, VEC, kBM, BK, PK>>::type;
+  using TileA = typename std::conditional<TA, Tile<T, VEC, BK, BM, kPitchM>, Tile<T, VEC, BM, BK, PK>>::type;
   using TileB = typename std::conditional<TB, Tile<T, VEC, BN, BK, PK>, Tile<T, VEC, BK, BN, kPitchN>>::type;
   __shared__ __attribute__((aligned(16))) T lds_a[2][TileA::kLdsElems];
   __shared__ __attribute__((aligned(16))) T lds_b[2][TileB::kLdsElems];
 
   // ---- tile of this block (XCD-aware, grouped) ----
-  const int tiles_m = (M + kBM - 1) / kBM, tiles_n = (N + BN - 1) / BN;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const int total = tiles_m * tiles_n;
   int bid = (int)blockIdx.x;
   // split-K (splits == 2, small grids): blocks [total, 2 total) take the
@@ -172,16 +178,16 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
   const int first_m = (bid / per_group) * kGroup;
   const int gsz = min(tiles_m - first_m, kGroup);
   const int tm = first_m + (bid % per_group) % gsz, tn = (bid % per_group) / gsz;
-  const int m0 = tm * kBM, n0 = tn * BN;
-  const bool interior = VEC && m0 + kBM <= M && n0 + BN <= N;  // (uniform)
+  const int m0 = tm * BM, n0 = tn * BN;
+  const bool interior = VEC && m0 + BM <= M && n0 + BN <= N;  // (uniform)
 
   const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * WN;
+  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * WN;
   const int fr = lane & 15, fk = lane >> 4;  // fragment: row/col within 16, k within 4
 
-  acc_t<T> acc[4][NT];
+  acc_t<T> acc[MI][NT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = acc_t<T>{0, 0, 0, 0};
 
@@ -245,15 +251,15 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
       // B's too from an [n][k] view) instead of four ds_read_b32
 #pragma unroll
       for (int kc = 0; kc < BK; kc += 16) {
-        f32x4 va[4], vb[NT];
+        f32x4 va[MI], vb[NT];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < MI; ++i) {
           const int m = wm + i * 16 + fr;
           if constexpr (!TA) {
             va[i] = *reinterpret_cast<const f32x4*>(&As[m * PK + kc + 4 * fk]);
           } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) va[i][e] = As[(kc + 4 * fk + e) * kPitchMN + m];
+            for (int e = 0; e < 4; ++e) va[i][e] = As[(kc + 4 * fk + e) * kPitchM + m];
           }
         }
 #pragma unroll
@@ -269,18 +275,18 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < NT; ++j) acc[i][j] = mfma((T)va[i][e], (T)vb[j][e], acc[i][j]);
       }
     } else {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
-      T fa[4], fb[NT];
+      T fa[MI], fb[NT];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < MI; ++i) {
         const int m = wm + i * 16 + fr, k = kk + fk;
-        fa[i] = TA ? As[k * kPitchMN + m] : As[m * PK + k];
+        fa[i] = TA ? As[k * kPitchM + m] : As[m * PK + k];
       }
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
@@ -288,7 +294,7 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
         fb[j] = TB ? Bs[n * PK + k] : Bs[k * kPitchN + n];
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
     }
@@ -298,7 +304,7 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
 
   // ---- epilogue: lanes 0..15 of a row are 16 consecutive columns ----
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < MI; ++i) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = m0 + wm + i * 16 + acc_row<T>(lane, r);
@@ -362,7 +368,14 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   const int occ = std::is_same<T, float>::value && bk == 16 ? (kOcc4 && eocc && atoi(eocc) == 4 ? 4 : 3) : 2;
   const bool nar = ebn ? atoi(ebn) == 64 : narrow_tiles(M, N, occ);
   const int bn = nar ? 64 : 128;
-  const int64_t tiles = (int64_t)((M + kBM - 1) / kBM) * ((N + bn - 1) / bn);
+  // 64 x 64 tiles when 128 x 64 ones would fill less than half the chip's
+  // workgroup slots (1024^3: 128 tiles for 512 / 768 slots); BK_GEMM_FP_BM=128
+  // turns it off
+  const char* ebm = getenv("BK_GEMM_FP_BM");
+  const int64_t tiles_n = (N + bn - 1) / bn;
+  const bool small = nar && occ < 4 && !(ebm && atoi(ebm) == 128) && 2 * ((M + kBM - 1) / kBM) * tiles_n < (int64_t)occ * kNumCU;
+  const int bm = small ? 64 : kBM;
+  const int64_t tiles = (int64_t)((M + bm - 1) / bm) * tiles_n;
   // split-K in two when the tiles fill at most half the chip's workgroup
   // slots and each half keeps >= 8 K tiles (1024^3 f32: 128 tiles on 768
   // slots); not for the gated fallback, whose C the split product wrote.
@@ -385,7 +398,10 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   const bool vf = getenv("BK_GEMM_FP_VEC") && atoi(getenv("BK_GEMM_FP_VEC")) != 0;
 #define BK_FP_LAUNCH(V, W, D, O)                                                                              \
   do {                                                                                                        \
-    if (vf && std::is_same<T, float>::value && (O) < 4) /* (at four per CU the vector reads spill) */          \
+    if (small && (W) == 64 && (O) < 4) /* (plain fragment reads) */                                          \
+      gemm_fp_kernel<T, TA, TB, V, W, D, O, false, 64><<<grid, kThreads, 0, stream>>>(                           \
+          (const T*)A, (const T*)B, (T*)C, M, N, K, lda, ldb, ldc, gate, splits);                                 \
+    else if (vf && std::is_same<T, float>::value && (O) < 4) /* (at four per CU the vector reads spill) */     \
       gemm_fp_kernel<T, TA, TB, V, W, D, O, std::is_same<T, float>::value && (O) < 4><<<grid, kThreads, 0,       \
                                                                                      stream>>>(                \
           (const T*)A, (const T*)B, (T*)C, M, N, K, lda, ldb, ldc, gate, splits);                                             \
@@ -567,8 +583,8 @@ BK_API int bk_gemm_fp(int dtype, int trans_a, int trans_b, const void* A, const 
   if (dtype != kF64 && dtype != kF32) return kBadArgument;
   if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0) return kBadArgument;
   if (lda < (trans_a ? M : K) || ldb < (trans_b ? K : N) || ldc < N) return kBadArgument;
-  const int64_t tiles = (int64_t)((M + fp::kBM - 1) / fp::kBM) * ((N + 63) / 64);  // (narrow tiles: 64 wide)
-  if (tiles > 0x7fffffffll) return kBadArgument;
+  const int64_t tiles = (int64_t)((M + 63) / 64) * ((N + 63) / 64);  // (the smallest tiles: 64 x 64)
+  if (2 * tiles > 0x7fffffffll) return kBadArgument;  // (split-K doubles the grid)
   const int es = dtype_size(dtype);
   const int e = 16 / es;
   const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % e == 0 && ldb % e == 0;
