@@ -24,6 +24,12 @@ constexpr int kShipped = g256::kOptRound1;
 // profiles/archive/r3_gemm_lab_spaced.log).
 constexpr long long kShippedW4 = g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore;
 constexpr int kW4MinK = 256;
+// ... and again from K = 18432 on: at long K the 8-wave kernel pulls ahead
+// (4096^2 x 24576: 611 vs 657 us, profiles/r5_gemm_longk_probe.jsonl; the
+// split f32 product's K' = 6 K: 4096^3 699 vs 780-786 us, 8192^3 5410 vs
+// 5864-5895, 3072^3 427 vs 436-450, r5_gemm_f32x6_w8.jsonl); at 16384 the
+// 4-wave one still leads (362 vs 419)
+constexpr int kW8MinK = 18432;
 
 bool gemm256_ok(int M, int N, int K, int lda, int ldb, int ldc, bool out_bf16) {
   return g256::ok(M, N, K, lda, ldb, ldc, out_bf16);
@@ -46,7 +52,7 @@ void launch_gemm256(const void* A, const void* Bt, void* C, int M, int N, int K,
                     float beta, bool out_bf16, hipStream_t stream, int which) {
   const bool w4_ok = g4::ok(M, N, K, lda, ldb, ldc, out_bf16);
   if (which == 0) which = forced_which();
-  if (which == 0) which = (w4_ok && K >= kW4MinK) ? 2 : 1;
+  if (which == 0) which = (w4_ok && K >= kW4MinK && K < kW8MinK) ? 2 : 1;
   if (which == 2 && w4_ok)
     g4::launch<kShippedW4>(A, Bt, C, M, N, K, lda, ldb, ldc, alpha, beta, out_bf16, stream);
   else
