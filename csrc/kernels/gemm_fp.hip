@@ -368,12 +368,20 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   const int occ = std::is_same<T, float>::value && bk == 16 ? (kOcc4 && eocc && atoi(eocc) == 4 ? 4 : 3) : 2;
   const bool nar = ebn ? atoi(ebn) == 64 : narrow_tiles(M, N, occ);
   const int bn = nar ? 64 : 128;
-  // 64 x 64 tiles when 128 x 64 ones would fill less than half the chip's
-  // workgroup slots (1024^3: 128 tiles for 512 / 768 slots); BK_GEMM_FP_BM=128
-  // turns it off
+  // 64 x 64 tiles: f64 wherever 64-wide tiles were chosen, f32 when 128 x 64
+  // ones would give the CUs fewer than two workgroups each (1024^3: 128
+  // tiles).  The small kernel holds 84-99 VGPRs and 38 KiB of LDS (f64; f32
+  // 43-53 and 20 KiB), so a CU runs four or more of its workgroups at once:
+  // f64 1536^3 227 -> 179 us, 3072^3 1074 -> 934, 4000x3000x1000 495 -> 427
+  // (f32 at 2048^3 / 3072^3: level or slower; f64 4096^3 / 8192^3 with
+  // square tiles stay ahead of 64 x 64 ones, 2083 vs 2174 us;
+  // profiles/r5_gemm_fp_bm64.jsonl).  BK_GEMM_FP_BM=128 turns it off, =64 on
+  // wherever the tiles are 64 wide (A/B runs).
   const char* ebm = getenv("BK_GEMM_FP_BM");
   const int64_t tiles_n = (N + bn - 1) / bn;
-  const bool small = nar && occ < 4 && !(ebm && atoi(ebm) == 128) && 2 * ((M + kBM - 1) / kBM) * tiles_n < (int64_t)occ * kNumCU;
+  const bool small = nar && occ < 4 &&
+                     (ebm ? atoi(ebm) == 64
+                          : std::is_same<T, double>::value || ((M + kBM - 1) / kBM) * tiles_n < 2 * kNumCU);
   const int bm = small ? 64 : kBM;
   const int64_t tiles = (int64_t)((M + bm - 1) / bm) * tiles_n;
   // split-K in two when the tiles fill at most half the chip's workgroup
