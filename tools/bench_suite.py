@@ -3,7 +3,8 @@
   1. hello_world on a CPU-only executor                  (--cpu-only)
   2. benchmark-fib on 1 GPU-pinned executor
   3. benchmark-numpy via HIP kernels on 1 GPU (headline)  + the unmodified
-     numpy payload on CPU in the same pod, and under the numpy offload
+     numpy payload on CPU in the same pod, and under the numpy offload;
+     likewise an unmodified numpy 4096^3 f64 matmul script
   4./5. (8 GPUs: 64 concurrent Executes, gang all-reduce) are the driver's
      N=8 bench.py run; on the 1-GPU box they are skipped.
 
@@ -27,6 +28,13 @@ RUNS = [
     # the same unmodified payload with the opt-in numpy offload (ops/numpy_offload.py)
     ("numpy_cpu_offload", ["--workload", "numpy_cpu", "--numpy-offload", "--steps", "30"]),
     ("scientific_gpu_pod", ["--workload", "scientific", "--steps", "30"]),
+    # unmodified numpy np.random.rand(4096, 4096) @ np.random.rand(4096, 4096)
+    # (examples/numpy_matmul_4096.py): OpenBLAS on the sandbox's CPUs, then
+    # the same script under the offload (the f64 MFMA GEMM)
+    ("numpy_matmul_cpu", ["--workload", "numpy_cpu", "--payload", "examples/numpy_matmul_4096.py", "--steps", "2",
+                          "--concurrency", "2"]),
+    ("numpy_matmul_offload", ["--workload", "numpy_cpu", "--payload", "examples/numpy_matmul_4096.py",
+                              "--numpy-offload", "--steps", "10"]),
 ]
 
 
