@@ -664,7 +664,7 @@ if rank == 0:
     env = {{k: v for k, v in sorted(os.environ.items()) if k.startswith(("NCCL_", "RCCL_"))}}
     ver = ".".join(map(str, torch.cuda.nccl.version())) if dev == "cuda" else None
     print(f"allreduce_ok={{ok}} busbw_GBps={{busbw:.1f}} small_us={{small_us:.1f}} init_ms={{(t_init - t0) * 1e3:.0f}}")
-    print("gang_sizes=" + json.dumps([[b, round(g, 2)] for b, g in sizes]))
+    print("gang_sizes=" + json.dumps([[b, float(format(g, ".4g"))] for b, g in sizes]))  # (4 digits: gloo on a busy CPU is < 0.01 GB/s)
     print("gang_env=" + json.dumps({{"backend": backend, "rccl_version": ver, "env": env}}))
 dist.destroy_process_group()
 """
