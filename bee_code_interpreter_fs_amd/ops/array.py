@@ -616,9 +616,9 @@ def _fp_dtype(x) -> bool:
 # bk_gemm_f32x6: f32-level error at the bf16 MFMA's rate) from 2^32
 # multiply-adds with M, N >= 256; smaller ones, and any product whose
 # workspace the HBM quota refuses, run on the f32 MFMA.  Measured medians
-# against the f32 kernel (profiles/r5_gemm_f32x6_bench.jsonl): 1024^3 80 vs
-# 51 us, 1536^3 113 vs 115, 2048^3 153 vs 156, 4096^3 785 vs 1044,
-# 8192^3 5905 vs 8126.  BEE_GEMM_F32X6: auto | 1 (whenever the shape allows)
+# against the f32 kernel, final tree (profiles/r5_gemm_fp_final.jsonl):
+# 1024^3 81 vs 33 us, 1536^3 113 vs 98, 2048^3 153 vs 161, 3072^3 430 vs
+# 595, 4096^3 696 vs 1084, 8192^3 5470 vs 8370.  BEE_GEMM_F32X6: auto | 1 (whenever the shape allows)
 # | 0 (never).
 _F32X6 = os.environ.get("BEE_GEMM_F32X6", "auto")
 _F32X6_MIN_MACS = 1 << 32
