@@ -50,16 +50,22 @@ void Admission::unmap_load_table() {
 }
 
 std::string Admission::refuse_reason(const JobClaim& c) const {
-  const int64_t hbm_room = lim_.hbm_capacity - lim_.standing_hbm;
+  // a gang's rank takes the place of the warm rank it runs as: while it runs,
+  // that rank's standing charge is its own HBM, not an extra (a gang holds
+  // its slots reserved, so nothing else is admitted beside it meanwhile)
+  const bool gang = c.ranks > 1;
+  const int64_t hbm_standing = std::max<int64_t>(lim_.standing_hbm - (gang ? lim_.standing_rank_hbm : 0), 0);
+  const int64_t hbm_room = lim_.hbm_capacity - hbm_standing;
   if (lim_.hbm_capacity > 0 && c.hbm > hbm_room)
     return "hbm_quota of " + std::to_string(c.hbm >> 20) + " MiB exceeds this GPU's usable HBM (" +
            std::to_string(std::max<int64_t>(hbm_room, 0) >> 20) + " MiB" +
-           (lim_.standing_hbm > 0 ? " after " + std::to_string(lim_.standing_hbm >> 20) + " MiB held by warm gang ranks"
-                                  : std::string()) +
+           (hbm_standing > 0 ? " after " + std::to_string(hbm_standing >> 20) + " MiB held by warm gang ranks"
+                             : std::string()) +
            ")";
   // a gang's ranks run on as many slots, each drained for it: N shares
   const int64_t ranks = std::max(1, c.ranks);
-  const int64_t mem_room = (lim_.mem_capacity - lim_.standing_mem) * ranks;
+  const int64_t mem_standing = std::max<int64_t>(lim_.standing_mem - (gang ? lim_.standing_rank_mem : 0), 0);
+  const int64_t mem_room = (lim_.mem_capacity - mem_standing) * ranks;
   if (lim_.mem_capacity > 0 && c.mem > mem_room)
     return "the job's sandbox memory bound (" + std::to_string(c.mem >> 20) + " MiB) exceeds its slots' " +
            "host-memory capacity (" + std::to_string(std::max<int64_t>(mem_room, 0) >> 20) + " MiB)";

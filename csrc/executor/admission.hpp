@@ -50,6 +50,10 @@ struct AdmissionLimits {
   int64_t mem_capacity = 0;   // bytes of host memory for this slot's sandbox trees; 0 = unbounded
   int64_t standing_hbm = 0;   // held by idle warm gang ranks on this GPU
   int64_t standing_mem = 0;
+  // one warm rank's share of them: a gang's rank runs as (replaces) the warm
+  // rank it takes, so a gang claim may use that rank's room too
+  int64_t standing_rank_hbm = 0;
+  int64_t standing_rank_mem = 0;
   double timeout_s = 900.0;   // longest wait for admission
 };
 

@@ -133,6 +133,29 @@ void standing_commitments() {
   a.finish(claim(7 << 20));
 }
 
+// a gang's rank runs as the warm rank it takes: its claim may use that rank's
+// share of the standing charge (counted once, not twice), a single job not
+void gang_rank_replaces_warm_rank() {
+  AdmissionLimits l = limits(0, 10 << 20, 10 << 20);
+  l.standing_hbm = 3 << 20;  // three warm ranks of 1 MiB
+  l.standing_mem = 3 << 20;
+  l.standing_rank_hbm = 1 << 20;
+  l.standing_rank_mem = 1 << 20;
+  Admission a(l);
+  JobClaim one = claim(8 << 20);
+  CHECK(!a.refuse_reason(one).empty());  // 8 > 10 - 3
+  JobClaim rank = claim(8 << 20);
+  rank.ranks = 2;
+  CHECK(a.refuse_reason(rank).empty());  // 8 <= 10 - (3 - 1)
+  rank.hbm = 9 << 20;
+  CHECK(a.refuse_reason(rank).find("2 MiB held by warm gang ranks") != std::string::npos);
+  JobClaim mem = claim(0, 16 << 20);
+  mem.ranks = 2;  // (10 - 2) x 2 ranks
+  CHECK(a.refuse_reason(mem).empty());
+  mem.mem = 17 << 20;
+  CHECK(!a.refuse_reason(mem).empty());
+}
+
 // a waiting job gives up at its deadline, and the tickets behind it move up
 void timeout() {
   AdmissionLimits l = limits(1);
@@ -273,6 +296,7 @@ int main(int argc, char** argv) {
     void (*fn)();
   } cases[] = {{"fifo_order", fifo_order},       {"hbm_commitment", hbm_commitment},
                {"mem_commitment", mem_commitment}, {"standing_commitments", standing_commitments},
+               {"gang_rank_replaces_warm_rank", gang_rank_replaces_warm_rank},
                {"timeout", timeout},             {"reservation", reservation},
                {"stopping", stopping},           {"stress", stress}};
   for (auto& c : cases) {

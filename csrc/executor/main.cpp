@@ -59,7 +59,8 @@ void usage() {
           "                    [--fault-spawn-fail-rate R]\n"
           "                    [--hbm-watchdog-ms MS] [--hbm-slack BYTES] [--max-inflight N] [--hbm-capacity BYTES]\n"
           "                    [--admit-timeout S] [--mem-capacity BYTES] [--sandbox-memory BYTES] [--sandbox-tasks N] [--sandbox-cpus C]\n"
-          "                    [--standing-hbm BYTES] [--standing-mem BYTES] [--gang-cpus GPU=LIST;...]\n"
+          "                    [--standing-hbm BYTES] [--standing-mem BYTES] [--standing-rank-hbm BYTES] [--standing-rank-mem BYTES]\n"
+          "                    [--gang-cpus GPU=LIST;...]\n"
           "                    [--monitor-ms MS] [--deny-ports P1,P2,...]\n"
           "                    [--cgroup auto|require|off|fake] [--cgroup-root DIR]\n");
 }
@@ -181,6 +182,8 @@ int main(int argc, char** argv) {
     else if (a == "--admit-timeout") cfg.admit_timeout_s = atof(val().c_str());
     else if (a == "--standing-hbm") cfg.standing_hbm = atoll(val().c_str());
     else if (a == "--standing-mem") cfg.standing_mem = atoll(val().c_str());
+    else if (a == "--standing-rank-hbm") cfg.standing_rank_hbm = atoll(val().c_str());
+    else if (a == "--standing-rank-mem") cfg.standing_rank_mem = atoll(val().c_str());
     else if (a == "--gang-cpus") {  // "0=0-15;1=16-31": each GPU's slot CPUs, for the gang ranks placed on it
       const std::string spec = val();
       size_t i = 0;

@@ -20,6 +20,8 @@ SandboxPool::SandboxPool(PoolConfig cfg) : cfg_(std::move(cfg)) {
   lim.mem_capacity = cfg_.mem_capacity;
   lim.standing_hbm = cfg_.hbm_capacity > 0 ? cfg_.standing_hbm : 0;
   lim.standing_mem = cfg_.mem_capacity > 0 ? cfg_.standing_mem : 0;
+  lim.standing_rank_hbm = cfg_.hbm_capacity > 0 ? cfg_.standing_rank_hbm : 0;
+  lim.standing_rank_mem = cfg_.mem_capacity > 0 ? cfg_.standing_rank_mem : 0;
   lim.timeout_s = cfg_.admit_timeout_s;
   admission_.reset(new Admission(lim));
 }

@@ -223,3 +223,62 @@ def test_automatic_tree_bound_splits_the_host_budget():
     assert lim["memory"] == 16 * GiB  # never above the slot's share: one sandbox always fits
     assert containment_limits(Config(_env={}, host_memory_budget_bytes=-1))["mem_capacity"] == 0
     assert containment_limits(Config(_env={}))["cpus"] == 8.0  # a default CPU share per sandbox
+
+
+def test_automatic_tree_bound_leaves_the_warm_gang_ranks_their_share():
+    """the automatic tree bound is derived from what the
+    slot's idle warm gang ranks leave of its host-memory share -- otherwise a
+    default request passes the front end and is refused by the daemon."""
+    from bee_code_interpreter_fs_amd.config import Config
+    from bee_code_interpreter_fs_amd.scheduler.local_gpu_pool import containment_limits
+
+    c = Config(_env={}, host_memory_budget_bytes=1024 * GiB, max_inflight_per_gpu=16)
+    lim = containment_limits(c, slots=8, standing_mem=3 * GiB)  # (128 - 3) GiB over 16
+    assert lim["mem_capacity"] == 128 * GiB and lim["memory"] == (125 * GiB) // 16
+    one = Config(_env={}, host_memory_budget_bytes=64 * GiB, max_inflight_per_gpu=1)
+    lim = containment_limits(one, slots=8, standing_mem=3 * GiB)  # 8 GiB per slot, 5 left, one sandbox
+    assert lim["memory"] == 5 * GiB and lim["memory"] + 3 * GiB <= lim["mem_capacity"]
+
+
+def test_default_quota_fits_beside_the_warm_gang_ranks():
+    """The default HBM quota x max in-flight fits what the warm gang ranks
+    leave of each GPU (8 GPUs, warm sets of 2, 4 and 8: three ranks per GPU)."""
+    from bee_code_interpreter_fs_amd.config import Config
+    from bee_code_interpreter_fs_amd.scheduler.local_gpu_pool import LocalGpuPoolBackend
+
+    for inflight in (1, 16):
+        c = Config(_env={}, max_inflight_per_gpu=inflight, gang_warm_sizes=[2, 4, 8])
+        b = LocalGpuPoolBackend(c, storage=None, gpu_ids=list(range(8)))
+        assert b.standing_hbm == 3 * c.gang_warm_rank_hbm_bytes
+        assert all(b._warm_ranks_on(i) == 3 for i in range(8))
+        assert b.default_quota * inflight + b.standing_hbm <= b.hbm_capacity
+        assert b.default_quota == (b.hbm_capacity - b.standing_hbm) // inflight
+    # no warm sets: the whole capacity
+    c = Config(_env={}, max_inflight_per_gpu=4, gang_warm_sizes=[])
+    b = LocalGpuPoolBackend(c, storage=None, gpu_ids=list(range(8)))
+    assert b.standing_hbm == 0 and b.default_quota == b.hbm_capacity // 4
+
+
+def test_one_inflight_job_per_gpu_with_warm_gang_ranks(tmp_path):
+    """max_inflight_per_gpu=1 on a 2-GPU node with a warm pair set: a
+    default-quota Execute and a gang of both GPUs both run (before the fix the
+    default quota was the whole capacity, which the daemon refused beside the
+    standing charge), and a request over what the warm ranks leave is refused
+    by the front end with the reason."""
+    h = ServiceHarness(str(tmp_path), gpu_ids=[0, 1], broker_enabled=False, worker_warm_gpu=False,
+                       workers_per_gpu_target=0, light_workers_per_gpu_target=1, min_workers_per_gpu_target=0,
+                       nano_workers_per_gpu_target=1, max_inflight_per_gpu=1, gang_warm_sizes=[2],
+                       gang_warm_rank_hbm_bytes=GiB, gang_warm_rank_memory_bytes=GiB, default_timeout=120.0)
+    h.start()
+    try:
+        b = h.ctx.code_executor
+        assert b.standing_hbm == GiB and b.default_quota == b.hbm_capacity - GiB
+        r = h.call(b.execute(source_code="print(6 * 7)"), timeout=120)
+        assert r.exit_code == 0 and r.stdout == "42\n", r.stderr
+        g = h.call(b.execute(source_code="import os; print(os.environ['RANK'])", gpus=2, nprocs=2, timeout=120),
+                   timeout=300)
+        assert g.exit_code == 0 and sorted(g.stdout.split()) == ["0", "1"], (g.stdout, g.stderr)
+        with pytest.raises(ValueError, match="warm gang ranks"):
+            h.call(b.execute(source_code="print(1)", hbm_bytes=b.hbm_capacity - GiB // 2), timeout=60)
+    finally:
+        h.stop()

@@ -13,7 +13,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "build", "sanitize", "bee-admission-test")
-CASES = ["fifo_order", "hbm_commitment", "mem_commitment", "standing_commitments", "timeout", "reservation",
+CASES = ["fifo_order", "hbm_commitment", "mem_commitment", "standing_commitments", "gang_rank_replaces_warm_rank", "timeout", "reservation",
          "stopping", "stress", "load_table"]
 
 

@@ -152,3 +152,48 @@ def test_a_grpc_peers_listener_is_tried_first_on_later_calls():
     finally:
         for x in (c, lo, hi):
             x.close()
+
+
+def test_socket_holder_asks_each_slot_with_a_time_limit(monkeypatch):
+    """one hung or dead daemon must not stall or refuse every
+    local caller.  A slot that hangs fails the lookup within the time limit
+    while its daemon lives (fail closed: it may run sandboxes); a dead
+    daemon's slot is skipped; a holder found on any slot wins."""
+    import asyncio
+    import time
+    from types import SimpleNamespace
+
+    from bee_code_interpreter_fs_amd.scheduler import local_gpu_pool as lgp
+
+    monkeypatch.setattr(lgp, "SOCKET_HOLDER_TIMEOUT_S", 0.2)
+
+    class Ex:
+        def __init__(self, reply=None, hang=False, alive=True):
+            self.reply, self.hang, self._alive = reply, hang, alive
+
+        async def get_json(self, path):
+            if self.hang:
+                await asyncio.sleep(30)
+            if isinstance(self.reply, Exception):
+                raise self.reply
+            return self.reply
+
+        def alive(self):
+            return self._alive
+
+    def backend(*exs):
+        b = object.__new__(lgp.LocalGpuPoolBackend)
+        b.slots = [SimpleNamespace(index=i, executor=e) for i, e in enumerate(exs)]
+        return b
+
+    run = lambda b: asyncio.run(b.socket_holder(7))  # noqa: E731
+    assert run(backend(Ex({}), Ex({"sandbox": True, "worker": "w9"}))) == "w9"
+    assert run(backend(Ex({}), Ex({}))) is None
+    t0 = time.monotonic()
+    with pytest.raises(RuntimeError, match="slot 1 did not answer"):
+        run(backend(Ex({}), Ex(hang=True)))
+    assert time.monotonic() - t0 < 2.0
+    # a dead daemon (hung or refusing) holds no sandbox: skipped
+    assert run(backend(Ex({}), Ex(hang=True, alive=False), Ex(ConnectionError("x"), alive=False))) is None
+    # a holder elsewhere is still found while another slot hangs
+    assert run(backend(Ex(hang=True), Ex({"sandbox": True, "worker": "w1"}))) == "w1"
