@@ -386,17 +386,48 @@ def idle_profile(service_pid, seconds: float):
                                                key=lambda kv: -kv[1])[:12])}
 
 
+_GPU_TIME: dict = {}  # slot_executions' last GPU-time read, by the list it returned
+
+
 def slot_executions(hport):
     """Executions so far of every GPU slot's daemon (for the per-slot
-    balance of the timed region)."""
+    balance of the timed region); the same status read's kernel-broker GPU
+    time (gpu_time_of) rides along."""
     import urllib.request
 
     try:
         with urllib.request.urlopen(f"http://127.0.0.1:{hport}/v1/status", timeout=10) as f:
             st = json.load(f)
-        return [int(s["executor"].get("executions", 0)) for s in st["slots"]]
+        out = [int(s["executor"].get("executions", 0)) for s in st["slots"]]
+        _GPU_TIME[id(out)] = [(s["executor"].get("broker") or {}) for s in st["slots"]]
+        return out
     except Exception:  # noqa: BLE001
         return None
+
+
+def gpu_time_of(slots0, slots1, total, elapsed):
+    """The GPU side of the timed window from the kernel brokers' event-timed
+    ops (csrc/executor/broker.cpp "GPU time per op"): per Execute, the busy
+    time (the union of the kernels' intervals on each GPU's clock: sessions
+    overlapping on one GPU count once) and the summed kernel durations; the
+    busy fraction of the window; and the rate the GPUs would allow at that
+    busy time per Execute, next to cpu_bound_rps (VERDICT r5 "next" #2)."""
+    b0, b1 = _GPU_TIME.get(id(slots0)), _GPU_TIME.get(id(slots1))
+    if not b0 or not b1 or len(b0) != len(b1) or not total or elapsed <= 0:
+        return None
+    if not all(x.get("gpu_timing") for x in b1):
+        return {"timing": "off"}
+    busy = sum(y.get("gpu_busy_ms", 0.0) - x.get("gpu_busy_ms", 0.0) for x, y in zip(b0, b1))
+    ops_ms = sum(y.get("gpu_op_ms", 0.0) - x.get("gpu_op_ms", 0.0) for x, y in zip(b0, b1))
+    ops = sum(y.get("gpu_ops", 0) - x.get("gpu_ops", 0) for x, y in zip(b0, b1))
+    per = busy / total
+    return {
+        "gpu_ms_per_exec": round(per, 4),           # busy GPU time per Execute (union of kernel intervals)
+        "kernel_ms_per_exec": round(ops_ms / total, 4),  # summed kernel durations (overlap counted twice)
+        "kernels_per_exec": round(ops / total, 2),
+        "gpu_utilisation": round(busy / (elapsed * 1e3 * len(b1)), 3),  # of the window, mean over GPUs
+        "gpu_bound_rps": round(len(b1) * 1e3 / per, 1) if per > 0 else None,
+    }
 
 
 def start_service(tmp: str, n_gpus: int, args):
@@ -1120,11 +1151,20 @@ def main():
                 bound["fraction_of_cpu_bound"] = round(out["value"] / cap, 3)
                 bound["bound_by"] = "cpu" if out["value"] >= 0.85 * cap or cpu_busy >= 0.9 * quota else \
                     "latency/gpu at this concurrency"
+            gt = gpu_time_of(slots0, slots1, total, max_elapsed) if rank == 0 else None
+            if gt is not None:
+                out["gpu_time"] = gt
+                if gt.get("gpu_bound_rps"):
+                    bound["gpu_bound_rps"] = gt["gpu_bound_rps"]
+                    bound["gpu_utilisation"] = gt["gpu_utilisation"]
+                    if "cpu_bound_rps" in bound and gt["gpu_bound_rps"] < bound["cpu_bound_rps"]:
+                        bound["bound_by"] = "gpu" if out["value"] >= 0.85 * gt["gpu_bound_rps"] else bound["bound_by"]
             out["node_bound"] = bound
             # next to the measured value: the rate this node's CPU quota allows
             # at the measured CPU per Execute -- a flat 1 -> N curve explains
             # itself when value sits at it
             out["cpu_bound_rps"] = bound.get("cpu_bound_rps")
+            out["gpu_bound_rps"] = bound.get("gpu_bound_rps")
             out["pss_mb"] = pss_by_role(svc_pid)
             if slots0 and slots1 and len(slots0) == len(slots1):
                 per_slot = [b - a for a, b in zip(slots0, slots1)]

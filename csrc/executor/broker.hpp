@@ -46,6 +46,16 @@ class KernelBroker {
   int64_t connections() const { return conns_.load(); }
   int64_t ops() const { return ops_.load(); }
   int64_t threads() const { return threads_.load(); }
+  // GPU time of the broker's kernels (event-timed per op, BEE_BROKER_GPU_TIMING,
+  // on by default): their summed durations, the union of their intervals on
+  // the GPU's clock (busy time: overlapping sessions count once) and how many
+  // ops, since start
+  struct GpuTime {
+    bool on = false;
+    double op_ms = 0, busy_ms = 0;
+    int64_t ops = 0;
+  };
+  GpuTime gpu_time() const;
 
  private:
   void accept_loop();

@@ -68,6 +68,11 @@ Json SandboxPool::status() {
     b.set("live_bytes", broker_->live_bytes());
     b.set("ops", broker_->ops());
     b.set("threads", broker_->threads());
+    const KernelBroker::GpuTime g = broker_->gpu_time();
+    b.set("gpu_timing", g.on);
+    b.set("gpu_op_ms", g.op_ms);    // summed event-timed durations of its kernels
+    b.set("gpu_busy_ms", g.busy_ms);  // the union of their intervals on the GPU clock
+    b.set("gpu_ops", g.ops);
     j.set("broker", b);
   }
   {

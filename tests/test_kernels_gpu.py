@@ -9,6 +9,8 @@ import os
 import numpy as np
 import pytest
 
+from .gemm_check import assert_gemm_close, gemm_error
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
@@ -209,9 +211,7 @@ def test_gemm_bf16(gpu, m, n, k, out_dtype):
     b_h = _bf16_round(rng.uniform(-1, 1, (k, n)).astype(np.float32))
     a, b = gpu.asarray(a_h, "bfloat16"), gpu.asarray(b_h, "bfloat16")
     c = gpu.matmul(a, b, out_dtype=out_dtype).numpy().astype(np.float64)
-    ref = a_h.astype(np.float64) @ b_h.astype(np.float64)
-    atol = 2e-3 * np.sqrt(k) if out_dtype == "float32" else 1e-2 * np.abs(ref).max()
-    np.testing.assert_allclose(c, ref, rtol=1e-2, atol=atol)
+    assert_gemm_close(c, a_h, b_h, out_dtype)
 
 
 def test_gemm_asymmetric_identity(gpu):
@@ -225,13 +225,42 @@ def test_gemm_asymmetric_identity(gpu):
     np.testing.assert_array_equal(ct, b_h)
 
 
+@pytest.mark.parametrize("out", ["float32", "bfloat16"])
+@pytest.mark.parametrize("shape", [(1024, 1024, 1024), (4096, 4096, 4096), (512, 768, 320)])
+def test_gemm_bound_catches_a_missing_k_tile(gpu, shape, out):
+    """The bound of tests/gemm_check.py is tight enough to matter: the same
+    kernel run one 64-deep K tile short of the operands fails it, the full
+    product passes (VERDICT r5 "next" #6)."""
+    import torch
+
+    from bee_code_interpreter_fs_amd.ops import _native
+
+    M, N, K = shape
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    bt = torch.empty(N, K, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1, generator=g)
+    dt = torch.float32 if out == "float32" else torch.bfloat16
+    lib = _native.lib()
+    s = torch.cuda.current_stream().cuda_stream
+    odt = 0 if out == "float32" else 2
+    full = torch.zeros(M, N, device="cuda", dtype=dt)
+    short = torch.zeros(M, N, device="cuda", dtype=dt)
+    assert lib.bk_gemm_bf16_tn_variant(a.data_ptr(), bt.data_ptr(), full.data_ptr(), M, N, K, K, K, N, 1.0, 0.0, odt,
+                                       0, s) == 0
+    assert lib.bk_gemm_bf16_tn_variant(a.data_ptr(), bt.data_ptr(), short.data_ptr(), M, N, K - 64, K, K, N, 1.0, 0.0,
+                                       odt, 0, s) == 0
+    torch.cuda.synchronize()
+    assert gemm_error(full, a, bt.T, out) <= 1.0
+    assert gemm_error(short, a, bt.T, out) > 10.0  # not a near miss
+
+
 def test_gemm_transposed_view_operand(gpu):
     rng = np.random.default_rng(11)
     a_h = _bf16_round(rng.uniform(-1, 1, (256, 512)).astype(np.float32))
     bt_h = _bf16_round(rng.uniform(-1, 1, (384, 512)).astype(np.float32))
     a, bt = gpu.asarray(a_h, "bfloat16"), gpu.asarray(bt_h, "bfloat16")
     c = gpu.matmul(a, bt.T, out_dtype="float32").numpy()
-    np.testing.assert_allclose(c, a_h.astype(np.float64) @ bt_h.T.astype(np.float64), rtol=1e-2, atol=5e-2)
+    assert_gemm_close(c, a_h, bt_h.T)
 
 
 @pytest.mark.parametrize("rows,cols,ld_in,ld_out", [
@@ -329,7 +358,7 @@ def test_matmul_wide_b_operand(gpu, b_kind):
     else:
         b = gpu.asarray(b_h, b_kind)
     c = gpu.matmul(gpu.asarray(a_h, "bfloat16"), b, out_dtype="float32").numpy()
-    np.testing.assert_allclose(c, a_h.astype(np.float64) @ b_h.astype(np.float64), rtol=1e-2, atol=2e-3 * 16)
+    assert_gemm_close(c, a_h, b_h)
 
 
 def test_matmul_row_major_b_large(gpu):
@@ -339,7 +368,7 @@ def test_matmul_row_major_b_large(gpu):
     a_h = _bf16_round(rng.uniform(-1, 1, (2048, 1024)).astype(np.float32))
     b_h = _bf16_round(rng.uniform(-1, 1, (1024, 4096)).astype(np.float32))
     c = gpu.matmul(gpu.asarray(a_h, "bfloat16"), gpu.asarray(b_h, "bfloat16"), out_dtype="float32").numpy()
-    np.testing.assert_allclose(c, a_h.astype(np.float64) @ b_h.astype(np.float64), rtol=1e-2, atol=2e-3 * 32)
+    assert_gemm_close(c, a_h, b_h)
 
 
 def test_quota_enforced(gpu):
@@ -394,9 +423,7 @@ def test_gemm_edge_kernel_unaligned_shapes(gpu, shape, out):
                                      0 if out == "float32" else 2, 0, torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     torch.cuda.synchronize()
-    ref = 0.75 * (a.double() @ bt.double().T) + 0.5 * c0[:, :N].double()
-    tol = 1e-3 if out == "float32" else 4e-2
-    assert (c[:, :N].double() - ref).abs().max().item() < tol * max(1.0, ref.abs().max().item())
+    assert_gemm_close(c[:, :N], a, bt.T, out, alpha=0.75, beta=0.5, c0=c0[:, :N])
     assert torch.equal(c[:, N:], c0[:, N:])  # masked stores: the padding columns are intact
 
 
@@ -424,7 +451,7 @@ def test_gemm_huge_leading_dimension(gpu):
                                          variant, torch.cuda.current_stream().cuda_stream)
         assert rc == 0, variant
         torch.cuda.synchronize()
-        assert (c.double() - ref).abs().max().item() < 1e-3 * max(1.0, ref.abs().max().item()), variant
+        assert gemm_error(c, a, bt.T) <= 1.0, variant
     del store
 
 
@@ -456,9 +483,7 @@ def test_gemm_256_edge_mode(gpu, shape, out, c_offset):
                                                torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     torch.cuda.synchronize()
-    ref = 0.75 * (a.double() @ bt.double().T) + 0.5 * c0[:, :N].double()
-    tol = 1e-3 if out == "float32" else 4e-2
-    assert (c[:, :N].double() - ref).abs().max().item() < tol * max(1.0, ref.abs().max().item())
+    assert_gemm_close(c[:, :N], a, bt.T, out, alpha=0.75, beta=0.5, c0=c0[:, :N])
     assert torch.equal(c[:, N:], c0[:, N:])
     assert torch.equal(store[:c_offset], store0[:c_offset]) and torch.equal(store[c_offset + M * ldc:],
                                                                           store0[c_offset + M * ldc:])
@@ -499,9 +524,7 @@ def test_gemm_kernel_variants_with_beta(gpu, variant, out):
     )
     assert rc == 0
     torch.cuda.synchronize()
-    ref = 0.75 * (a.double() @ bt.double().T) + 0.5 * c0.double()
-    tol = 1e-3 if out == "float32" else 4e-2
-    assert (c.double() - ref).abs().max().item() < tol * max(1.0, ref.abs().max().item())
+    assert_gemm_close(c, a, bt.T, out, alpha=0.75, beta=0.5, c0=c0)
 
 
 def test_preload_loads_every_kernel_module(gpu):
@@ -605,9 +628,7 @@ def test_gemm_nn_kernel(gpu, shape, out, pad):
                              torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     torch.cuda.synchronize()
-    ref = 0.75 * (a.double() @ b.double()) + 0.5 * c0.double()
-    tol = 1e-3 if out == "float32" else 4e-2
-    assert (c.double() - ref).abs().max().item() < tol * max(1.0, ref.abs().max().item())
+    assert_gemm_close(c, a, b, out, alpha=0.75, beta=0.5, c0=c0)
 
 
 def test_gemm_nn_refuses_what_it_cannot_do(gpu):
@@ -643,8 +664,7 @@ def test_matmul_row_major_b(gpu, nn, monkeypatch):
         c = gpu.matmul(a, b, out_dtype="float32").numpy()
         ab = a.astype("float32").numpy().astype(np.float64)
         bb = b.astype("float32").numpy().astype(np.float64)
-        ref = ab @ bb
-        assert np.abs(c - ref).max() < 1e-3 * max(1.0, np.abs(ref).max()), (M, N, K)
+        assert gemm_error(c, ab, bb) <= 1.0, (M, N, K)
 
 
 @pytest.mark.parametrize("n", [1, 2, 5, 8, 16])
@@ -662,9 +682,7 @@ def test_gemv_shapes_take_the_skinny_kernel(gpu, n, out):
     lib = _native.lib()
     assert lib.bk_gemm_bf16_pick(a.ptr, bt.ptr, a.ptr, m, n, k, k, k, n, 0 if out == "float32" else 2) == 8
     c = gpu.gemm_bf16_tn(a, bt, out_dtype=out).numpy().astype(np.float64)
-    ref = a_h.astype(np.float64) @ bt_h.astype(np.float64).T
-    atol = 2e-3 * np.sqrt(k) if out == "float32" else 1e-2 * np.abs(ref).max()
-    np.testing.assert_allclose(c, ref, rtol=1e-2, atol=atol)
+    assert_gemm_close(c, a_h, bt_h.T, out)
 
 
 def test_headline_gemm_check_catches_one_corrupt_tile(gpu):

@@ -33,6 +33,29 @@ def test_payload_runs_on_pinned_gpu(gsvc):
     assert r.gpu_ids == [0]
 
 
+def test_broker_times_its_kernels_on_the_gpu_clock(gsvc):
+    """The kernel broker's event-timed ops (csrc/executor/broker.cpp "GPU
+    time per op", reported by bench.py as gpu_ms_per_exec): one headline
+    payload adds its ~10 kernels, their summed durations include the 4096^3
+    GEMM (>= 40 us at any sane clock) and the busy union of one sandbox's
+    serial stream equals that sum."""
+    import os
+
+    ex = gsvc.ctx.code_executor.slots[0].executor
+    b0 = gsvc.call(ex.get_json("/v1/status"))["broker"]
+    assert b0["gpu_timing"] is True
+    src = open(os.path.join(os.path.dirname(__file__), "..", "examples", "benchmark_numpy_gpu.py")).read()
+    r = run(gsvc, src)
+    assert r.exit_code == 0, r.stderr
+    b1 = gsvc.call(ex.get_json("/v1/status"))["broker"]
+    ops = b1["gpu_ops"] - b0["gpu_ops"]
+    op_ms = b1["gpu_op_ms"] - b0["gpu_op_ms"]
+    busy = b1["gpu_busy_ms"] - b0["gpu_busy_ms"]
+    assert 6 <= ops <= 40, ops
+    assert 0.04 <= op_ms <= 50.0, op_ms
+    assert busy <= op_ms * 1.001 + 1e-3 and busy >= 0.9 * op_ms, (busy, op_ms)
+
+
 def test_nano_sandbox_runs_beekern_without_numpy(gsvc):
     """A beekern + stdlib script lands in a nano sandbox (zygote without
     numpy, python -S): the broker path works, reductions come back as plain

@@ -31,7 +31,7 @@ import json, sys
 d = json.loads(sys.argv[1]); s = d['executors'][0].get('sandbox_cpu', {})
 print(json.dumps({'variant': sys.argv[2], 'round': int(sys.argv[3]), 'value': d['value'], 'p50': d['p50_latency_ms'],
                   'errors': d['errors'], 'cpu_ms_per_exec': d.get('cpu_ms_per_exec'), 'sandbox_cpu': s,
-                  'p50_phase_ms': d.get('p50_phase_ms'), 'node_bound': d.get('node_bound')}))
+                  'p50_phase_ms': d.get('p50_phase_ms'), 'node_bound': d.get('node_bound'), 'gpu_time': d.get('gpu_time')}))
 " "$line" "$name" "$round" >> $OUT
   done
 done
