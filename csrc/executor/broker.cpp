@@ -87,75 +87,56 @@ class HipDevice final : public broker::Device {
     std::vector<std::pair<hipEvent_t, void*>> pending;
     std::vector<hipEvent_t> spare_events;
     hipEvent_t wait_ev = nullptr;
-    // GPU timing: (start, end) event pairs of launched ops not yet harvested
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;
-    std::vector<hipEvent_t> spare_timing;
+    // GPU timing: the open segment's start (the first op launched since the
+    // last wait), ops launched in it
+    hipEvent_t seg_start = nullptr;
+    bool seg_open = false;
+    int64_t seg_ops = 0;
   };
 
-  // ---- GPU time per op -------------------------------------------------------
+  // ---- GPU time per segment ---------------------------------------------------
   //
-  // Each kernel op is bracketed by two timing events on its stream; once the
-  // session has waited for its stream (every reduce / read does) or ends, the
-  // pairs are harvested: their durations are summed, and their intervals --
-  // on the GPU's own clock, against a reference event re-recorded every
-  // second so float milliseconds stay precise -- are merged into the GPU's
-  // busy time, which counts overlapping sessions once.  bench.py reports
-  // both per Execute next to the CPU budget (VERDICT r5 "next" #2: the
-  // driver's GPU-busy sampler cannot see a 50 ms window).
-  // BEE_BROKER_GPU_TIMING=0: off (two event records per op less).
-  hipEvent_t timing_event(Ctx* c) {
-    if (!c->spare_timing.empty()) {
-      hipEvent_t e = c->spare_timing.back();
-      c->spare_timing.pop_back();
-      return e;
-    }
-    hipEvent_t e = nullptr;
-    return hipEventCreateWithFlags(&e, hipEventDefault) == hipSuccess ? e : nullptr;
-  }
+  // A session's ops run in order on its stream, and it waits for the stream
+  // whenever it needs a result (every reduce / read).  So the GPU time of its
+  // work is the segments between waits: one timing event where a segment's
+  // first op is launched, and the wait's own event (timing-enabled) where it
+  // ends -- two event reads per wait, not two records and reads per op (that
+  // cost 0.13 ms of daemon CPU per headline Execute, profiles/r6_gpu_timing_ab.jsonl).
+  // The segments' durations are summed, and their intervals -- on the GPU's
+  // own clock, against a reference event re-recorded every second so float
+  // milliseconds stay precise -- are merged into the GPU's busy time, which
+  // counts overlapping sessions once.  bench.py reports both per Execute next
+  // to the CPU budget (VERDICT r5 "next" #2: the driver's GPU-busy sampler
+  // cannot see a 50 ms window).  A segment also spans a copy queued in it and
+  // any idle gap between its last launch and the wait (microseconds: the
+  // payloads launch and then wait).  BEE_BROKER_GPU_TIMING=0: off.
   template <typename F>
   int timed(void* s, hipStream_t q, F&& launch) {
     if (!timing_) return launch(q);
     Ctx* c = (Ctx*)s;
-    hipEvent_t e0 = timing_event(c);
-    if (e0 && hipEventRecord(e0, q) != hipSuccess) {
-      c->spare_timing.push_back(e0);
-      e0 = nullptr;
+    if (!c->seg_open) {
+      if (!c->seg_start && hipEventCreateWithFlags(&c->seg_start, hipEventDefault) != hipSuccess) c->seg_start = nullptr;
+      c->seg_open = c->seg_start && hipEventRecord(c->seg_start, q) == hipSuccess;
+      c->seg_ops = 0;
     }
     const int rc = launch(q);
-    if (!e0) return rc;
-    hipEvent_t e1 = timing_event(c);
-    if (rc != 0 || !e1 || hipEventRecord(e1, q) != hipSuccess) {
-      c->spare_timing.push_back(e0);
-      if (e1) c->spare_timing.push_back(e1);
-      return rc;
-    }
-    c->timed.emplace_back(e0, e1);
+    if (rc == 0) c->seg_ops++;
     return rc;
   }
-  // after a completed wait (all: the stream is drained) or at session end
-  void harvest(Ctx* c) {
-    if (c->timed.empty()) return;
+  // after a completed wait on `end` (a timing event behind everything the
+  // segment launched): close the segment
+  void harvest(Ctx* c, hipEvent_t end) {
+    if (!c->seg_open) return;
+    c->seg_open = false;
     std::lock_guard<std::mutex> lk(time_mu_);
     rebase_locked();
-    size_t keep = 0;
-    for (size_t i = 0; i < c->timed.size(); ++i) {
-      auto& pr = c->timed[i];
-      if (hipEventQuery(pr.second) != hipSuccess) {
-        c->timed[keep++] = pr;
-        continue;
-      }
-      float t0 = 0, t1 = 0, dur = 0;
-      if (hipEventElapsedTime(&t0, ref_, pr.first) == hipSuccess &&
-          hipEventElapsedTime(&t1, ref_, pr.second) == hipSuccess &&
-          hipEventElapsedTime(&dur, pr.first, pr.second) == hipSuccess) {
-        op_ms_ += dur;
-        ops_timed_++;
-        spans_.push_back({ref_base_ms_ + t0, ref_base_ms_ + t0 + dur});
-      }
-      c->spare_timing.push_back(pr.first);
-      c->spare_timing.push_back(pr.second);
+    float t0 = 0, dur = 0;
+    if (hipEventElapsedTime(&t0, ref_, c->seg_start) == hipSuccess &&
+        hipEventElapsedTime(&dur, c->seg_start, end) == hipSuccess && dur >= 0) {
+      op_ms_ += dur;
+      ops_timed_ += c->seg_ops;
+      spans_.push_back({ref_base_ms_ + t0, ref_base_ms_ + t0 + dur});
     }
-    c->timed.resize(keep);
     if (spans_.size() > 65536) fold_locked();
   }
   // a fresh reference event once a second (float ms lose precision as they
@@ -228,12 +209,19 @@ class HipDevice final : public broker::Device {
   // at most 1/4.  BEE_BROKER_POLL tunes it, BEE_BROKER_WAIT=spin: HIP's wait.
   bool wait(Ctx* c) {
     const bool ok = wait_stream(c);
-    if (ok) harvest(c);
+    if (ok && c->seg_open) {
+      if (c->wait_ev && !spin_wait_) {
+        harvest(c, c->wait_ev);
+      } else {
+        c->seg_open = false;  // (no timed end event: the segment is not counted)
+      }
+    }
     return ok;
   }
   bool wait_stream(Ctx* c) {
     if (spin_wait_) return hipStreamSynchronize(c->s) == hipSuccess;
-    if (!c->wait_ev && hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming) != hipSuccess)
+    // (timing-enabled when the broker times segments: the wait's event ends one)
+    if (!c->wait_ev && hipEventCreateWithFlags(&c->wait_ev, timing_ ? hipEventDefault : hipEventDisableTiming) != hipSuccess)
       return hipStreamSynchronize(c->s) == hipSuccess;
     if (hipEventRecord(c->wait_ev, c->s) != hipSuccess) return false;
     long ns = poll_min_ns_;
@@ -392,7 +380,7 @@ class HipDevice final : public broker::Device {
     bk.malloc_(&c->scalar, 256);
     void* page = nullptr;
     if (hipHostMalloc(&page, 64, hipHostMallocCoherent) == hipSuccess) c->slot = (double*)page;
-    hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming);
+    hipEventCreateWithFlags(&c->wait_ev, timing_ ? hipEventDefault : hipEventDisableTiming);
     for (int i = 0; i < 4; ++i) {  // the deferred-free events a session typically has in flight
       hipEvent_t ev = nullptr;
       if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) c->spare_events.push_back(ev);
@@ -402,7 +390,7 @@ class HipDevice final : public broker::Device {
   void give_stream(void* p) override {
     Ctx* c = (Ctx*)p;
     reap(c, true);  // the session drained the stream before handing it back
-    harvest(c);
+    if (c->seg_open) wait(c);  // (launches after its last wait: close that segment)
     std::lock_guard<std::mutex> lk(mu_);
     pool_.push_back(c);
   }
