@@ -54,7 +54,7 @@ void usage() {
           "                    [--broker-lib SO] [--light-target N] [--light-zygotes N] [--light-preload MODS]\n"
           "                    [--min-target N] [--min-zygotes N] [--min-preload MODS] [--min-cpu-target N]\n"
           "                    [--workspace DIR] [--runtime-packages DIR] [--die-with-parent 0|1]\n"
-          "                    [--jail 0|1] [--uid-base UID] [--uid-count N] [--protect DIR]... [--nproc N]\n"
+          "                    [--jail 0|1] [--listen-guard 0|1] [--uid-base UID] [--uid-count N] [--protect DIR]... [--nproc N]\n"
           "                    [--mem-limit BYTES] [--cpus LIST] [--gang-grace S]\n"
           "                    [--fault-spawn-fail-rate R]\n"
           "                    [--hbm-watchdog-ms MS] [--hbm-slack BYTES] [--max-inflight N] [--hbm-capacity BYTES]\n"
@@ -183,6 +183,7 @@ int main(int argc, char** argv) {
     else if (a == "--standing-hbm") cfg.standing_hbm = atoll(val().c_str());
     else if (a == "--standing-mem") cfg.standing_mem = atoll(val().c_str());
     else if (a == "--standing-rank-hbm") cfg.standing_rank_hbm = atoll(val().c_str());
+    else if (a == "--listen-guard") cfg.listen_guard = val() != "0";
     else if (a == "--standing-rank-mem") cfg.standing_rank_mem = atoll(val().c_str());
     else if (a == "--gang-cpus") {  // "0=0-15;1=16-31": each GPU's slot CPUs, for the gang ranks placed on it
       const std::string spec = val();
