@@ -582,7 +582,7 @@ class HipDevice final : public broker::Device {
   // Round 5: each check 1/4 of the wait so far after the last (was 1/8):
   // 600-step headline A/B, 2 interleaved rounds on one box, daemon CPU
   // 0.665 / 0.673 vs 0.700 / 0.690 ms per Execute, RPS 3328 / 3280 vs 3300 /
-  // 3247; 1/2 lost throughput (3092 / 3185) (profiles/r5_broker_poll_ab.jsonl).
+  // 3247; 1/2 lost throughput (3092 / 3185) (profiles/archive/r5_broker_poll_ab.jsonl).
   long poll_min_ns_ = 2000, poll_max_ns_ = 500000;
   int poll_div_ = 4;
   bool poll_set_ = (poll_schedule(&poll_min_ns_, &poll_max_ns_, &poll_div_), true);

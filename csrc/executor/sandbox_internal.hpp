@@ -35,7 +35,9 @@ extern char** environ;
 namespace bee {
 namespace sandbox_detail {
 
-inline bool read_line(int fd, std::string& buf, std::string* line) {
+// the next line of `fd`; with `fds`, descriptors passed along (SCM_RIGHTS)
+// are collected there (read() would drop them)
+inline bool read_line(int fd, std::string& buf, std::string* line, std::vector<int>* fds = nullptr) {
   while (true) {
     size_t nl = buf.find('\n');
     if (nl != std::string::npos) {
@@ -44,7 +46,27 @@ inline bool read_line(int fd, std::string& buf, std::string* line) {
       return true;
     }
     char tmp[8192];
-    ssize_t r = read(fd, tmp, sizeof tmp);
+    ssize_t r;
+    if (fds) {
+      alignas(cmsghdr) char cbuf[CMSG_SPACE(4 * sizeof(int))];
+      iovec iov{tmp, sizeof tmp};
+      msghdr mh{};
+      mh.msg_iov = &iov;
+      mh.msg_iovlen = 1;
+      mh.msg_control = cbuf;
+      mh.msg_controllen = sizeof cbuf;
+      r = recvmsg(fd, &mh, MSG_CMSG_CLOEXEC);
+      if (r >= 0)
+        for (cmsghdr* cm = CMSG_FIRSTHDR(&mh); cm; cm = CMSG_NXTHDR(&mh, cm))
+          if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_RIGHTS)
+            for (size_t k = 0; k < (cm->cmsg_len - CMSG_LEN(0)) / sizeof(int); ++k) {
+              int pf;
+              memcpy(&pf, CMSG_DATA(cm) + k * sizeof(int), sizeof pf);
+              fds->push_back(pf);
+            }
+    } else {
+      r = read(fd, tmp, sizeof tmp);
+    }
     if (r < 0 && errno == EINTR) continue;
     if (r <= 0) return false;
     buf.append(tmp, (size_t)r);

@@ -94,6 +94,7 @@ std::shared_ptr<Worker> SandboxPool::spawn_worker(bool pooled, int kind, const s
   }
   w->id = fixed_id.empty() ? "w" + random_hex(6) : fixed_id;
   w->pooled = pooled;
+  w->gang_rank = gang_rank;
   w->kind = kind;
   w->gpus = gpus;
   w->set_quota(cfg_.default_hbm_quota);

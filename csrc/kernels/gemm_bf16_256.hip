@@ -25,7 +25,7 @@ constexpr int kShipped = g256::kOptRound1;
 constexpr long long kShippedW4 = g4::kAsmMfma | g4::kInterleave | g4::kTwoBar | g4::kTwoBarG10 | g4::kNtStore;
 constexpr int kW4MinK = 256;
 // ... and again from K = 18432 on: at long K the 8-wave kernel pulls ahead
-// (4096^2 x 24576: 611 vs 657 us, profiles/r5_gemm_longk_probe.jsonl; the
+// (4096^2 x 24576: 611 vs 657 us, profiles/archive/r5_gemm_longk_probe.jsonl; the
 // split f32 product's K' = 6 K: 4096^3 699 vs 780-786 us, 8192^3 5410 vs
 // 5864-5895, 3072^3 427 vs 436-450, r5_gemm_f32x6_w8.jsonl); at 16384 the
 // 4-wave one still leads (362 vs 419)

@@ -34,7 +34,7 @@
 //
 // Small products (fewer 128 x 64 tiles than half the chip's workgroup slots)
 // take 64 x 64 tiles and, while still at most half full, a deterministic
-// two-way split-K (profiles/r5_gemm_fp_bm64.jsonl, r5_gemm_fp_splitk.jsonl).
+// two-way split-K (profiles/archive/r5_gemm_fp_bm64.jsonl, r5_gemm_fp_splitk.jsonl).
 //
 // Any M, N, K and leading dimensions: out-of-range elements load as zero and
 // stores are masked; 16-B loads where pointers and leading dimensions allow,
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
 // rounds, and a last round that is mostly empty idles the CUs for a whole
 // tile's time.  4000 x 3000 f64 at 2 per CU: 768 square tiles = 1.5 rounds
 // (0.75 of the slots busy) vs 1504 narrow ones = 2.94 (0.98): 66% -> 74% of
-// torch.matmul (profiles/r5_gemm_fp_bench.jsonl, r5_gemm_fp_tiles.jsonl).
+// torch.matmul (profiles/archive/r5_gemm_fp_bench.jsonl, r5_gemm_fp_tiles.jsonl).
 // Small products (fewer square tiles than two per CU) always go narrow.
 inline double round_fill(int64_t tiles, int64_t slots) {
   const int64_t rounds = (tiles + slots - 1) / slots;
@@ -361,7 +361,7 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   // f32 at 16 deep: three workgroups per CU.  Four fit too (<= 128 VGPRs,
   // 38 KiB of LDS each; not A . B^T, whose [n][k] B reads then spill), but
   // measured level with three: 4096^3 0.884 vs 0.885 of torch.matmul, 8192^3
-  // 0.881 both (profiles/r5_gemm_fp_occ.jsonl) -- the waves' fragment-read
+  // 0.881 both (profiles/archive/r5_gemm_fp_occ.jsonl) -- the waves' fragment-read
   // waits after each barrier, not the slot count, hold it.  BK_GEMM_FP_OCC=4.
   const char* eocc = getenv("BK_GEMM_FP_OCC");
   constexpr bool kOcc4 = !(!TA && TB);
@@ -375,7 +375,7 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   // f64 1536^3 227 -> 179 us, 3072^3 1074 -> 934, 4000x3000x1000 495 -> 427
   // (f32 at 2048^3 / 3072^3: level or slower; f64 4096^3 / 8192^3 with
   // square tiles stay ahead of 64 x 64 ones, 2083 vs 2174 us;
-  // profiles/r5_gemm_fp_bm64.jsonl).  BK_GEMM_FP_BM=128 turns it off, =64 on
+  // profiles/archive/r5_gemm_fp_bm64.jsonl).  BK_GEMM_FP_BM=128 turns it off, =64 on
   // wherever the tiles are 64 wide (A/B runs).
   const char* ebm = getenv("BK_GEMM_FP_BM");
   const int64_t tiles_n = (N + bn - 1) / bn;

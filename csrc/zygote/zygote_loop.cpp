@@ -375,7 +375,7 @@ void kill_escapees(const std::unordered_set<pid_t>& children) {
 // The pooled phase's own faults are off the request path anyway, and copying
 // them up front saved no CPU on the MI355X box: a populated page cost what
 // its fault did (~1.1 us).  600-step headline runs, interleaved on one box
-// (profiles/r5_cow_prefault_ab.jsonl): request-path set 3413 / 3449 RPS,
+// (profiles/archive/r5_cow_prefault_ab.jsonl): request-path set 3413 / 3449 RPS,
 // full set (BEE_COW_PREFAULT=2) 3352 / 3451, off 3221 / 3180; sandbox CPU
 // per Execute 2.71 / 2.65-2.67 / 2.58-2.62 ms (an earlier box: full set
 // +0.1-0.5 ms over off).  BEE_COW_PREFAULT=0: off.
@@ -439,7 +439,7 @@ using PageList = std::vector<uint64_t, MapAlloc<uint64_t>>;
 // 1.32-1.34 ms per sandbox without the prefault).  So each spawn profile
 // learns and prefaults its own set (then: hello 1.59-1.63 vs 1.34-1.42 ms,
 // the request path's own pages; headline 3294 / 3260 vs 3010 / 3008 RPS,
-// profiles/r5_cow_profiles_ab.jsonl).
+// profiles/archive/r5_cow_profiles_ab.jsonl).
 constexpr int kCowProfiles = 2;  // 0: eager broker session, 1: lazy (BEE_BROKER_LAZY=1)
 
 struct CowProfile {
