@@ -76,6 +76,7 @@ Json SandboxPool::status() {
       g.set("parked", gs.parked);
       g.set("exempt", gs.exempt);
       g.set("errors", gs.errors);
+      g.set("last_refused", gs.last_refused);
     } else {
       g.set("why", guard_why_);
     }
