@@ -75,6 +75,7 @@ Json SandboxPool::status() {
       g.set("eagain", gs.eagain);
       g.set("parked", gs.parked);
       g.set("exempt", gs.exempt);
+      g.set("closed_peers", gs.closed_peers);
       g.set("errors", gs.errors);
       g.set("last_refused", gs.last_refused);
     } else {
