@@ -613,15 +613,15 @@ def _fp_dtype(x) -> bool:
 
 
 # f32 products take the six-piece bf16 split (csrc/kernels/gemm_fp.hip
-# bk_gemm_f32x6: f32-level error at the bf16 MFMA's rate) from 2^32
+# bk_gemm_f32x6: f32-level error at the bf16 MFMA's rate) above 2^33
 # multiply-adds with M, N >= 256; smaller ones, and any product whose
-# workspace the HBM quota refuses, run on the f32 MFMA.  Measured medians
-# against the f32 kernel, final tree (profiles/r5_gemm_fp_final.jsonl):
-# 1024^3 81 vs 33 us, 1536^3 113 vs 98, 2048^3 153 vs 161, 3072^3 430 vs
-# 595, 4096^3 696 vs 1084, 8192^3 5470 vs 8370.  BEE_GEMM_F32X6: auto | 1 (whenever the shape allows)
-# | 0 (never).
+# workspace the HBM quota refuses, run on the f32 MFMA.  Measured medians,
+# split vs f32 kernel (profiles/r6_gemm_fp_sweep.jsonl): 1024^3 81 vs 25 us,
+# 1536^3 113 vs 79, 2048^3 (= 2^33) 153 vs 143, 4000x3000x1000 153 vs 230,
+# 3072^3 426 vs 604, 4096^3 696 vs 1088.  BEE_GEMM_F32X6: auto | 1 (whenever
+# the shape allows) | 0 (never).
 _F32X6 = os.environ.get("BEE_GEMM_F32X6", "auto")
-_F32X6_MIN_MACS = 1 << 32
+_F32X6_MIN_MACS = (1 << 33) + 1
 
 
 def f32x6_workspace_bytes(M: int, N: int, K: int) -> int:

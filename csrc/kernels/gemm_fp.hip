@@ -33,8 +33,9 @@
 //    panels and B column panels a group shares stay in that XCD's L2).
 //
 // Small products (fewer 128 x 64 tiles than half the chip's workgroup slots)
-// take 64 x 64 tiles and, while still at most half full, a deterministic
-// two-way split-K (profiles/archive/r5_gemm_fp_bm64.jsonl, r5_gemm_fp_splitk.jsonl).
+// take 64-row tiles and, while still at most half full, two K groups per
+// workgroup whose halves meet in LDS (deterministic, no C memset;
+// profiles/archive/r5_gemm_fp_bm64.jsonl, r5_gemm_fp_splitk.jsonl).
 //
 // Any M, N, K and leading dimensions: out-of-range elements load as zero and
 // stores are masked; 16-B loads where pointers and leading dimensions allow,
@@ -80,25 +81,32 @@ __device__ __forceinline__ int acc_row(int lane, int r) {
 
 // One operand tile: `ROWS` x `COLS` elements of a row-major buffer starting
 // at (r0, c0), copied to LDS in the same orientation as 16-B chunks (LDS row
-// pitch PITCH elements).  An A tile is 128 x BK ([m][k]) or BK x 128
-// ([k][m]); a B tile BK x BN or BN x BK.  Chunks are spread evenly over the
-// 256 threads (consecutive threads take consecutive chunks of a row: every
-// 16-B load of a wave lands in whole 64-B segments).
+// pitch PITCH elements).  An A tile is BM x BK ([m][k]) or BK x BM ([k][m]);
+// a B tile BK x BN or BN x BK.  Chunks are spread evenly over the 256 threads
+// of one K group (`tid`; consecutive threads take consecutive chunks of a row:
+// every 16-B load of a wave lands in whole 64-B segments); a tile of fewer
+// chunks than threads (16 x 32 f32) leaves the last threads idle.
 template <typename T, bool VEC, int ROWS, int COLS, int PITCH>
 struct Tile {
   static constexpr int E = 16 / sizeof(T);  // elements per 16-B chunk
   static constexpr int CPR = COLS / E;      // chunks per tile row
-  static constexpr int kChunks = ROWS * CPR / kThreads;
-  static_assert(ROWS * CPR % kThreads == 0, "whole chunks per thread");
+  static constexpr int kTotal = ROWS * CPR;
+  static constexpr int kChunks = (kTotal + kThreads - 1) / kThreads;
+  static constexpr bool kPartial = kTotal % kThreads != 0;
+  static_assert(!kPartial || kTotal < kThreads, "whole chunks per thread, or one chunk for some threads");
   static constexpr int kLdsElems = ROWS * PITCH;
+  static_assert(kLdsElems * sizeof(T) % 16 == 0, "16-B aligned LDS stages");
   T v[kChunks][E];
 
+  __device__ __forceinline__ static bool owns(int q) { return !kPartial || q < kTotal; }
+
   // every element in range (an interior tile): 16-B loads, no guards
-  __device__ __forceinline__ void load_fast(const T* __restrict__ g, int64_t ld, int r0, int c0) {
+  __device__ __forceinline__ void load_fast(const T* __restrict__ g, int64_t ld, int r0, int c0, int tid) {
     const T* base = g + (int64_t)r0 * ld + c0;
 #pragma unroll
     for (int c = 0; c < kChunks; ++c) {
-      const int q = c * kThreads + (int)threadIdx.x;
+      const int q = c * kThreads + tid;
+      if (!owns(q)) continue;
       const u32x4_t w = *reinterpret_cast<const u32x4_t*>(base + (int64_t)(q / CPR) * ld + (q % CPR) * E);
       __builtin_memcpy(v[c], &w, 16);
     }
@@ -106,10 +114,11 @@ struct Tile {
 
   // edge tiles: out-of-range elements are zero
   __device__ __forceinline__ void load_guarded(const T* __restrict__ g, int64_t ld, int row_end, int col_end, int r0,
-                                               int c0) {
+                                               int c0, int tid) {
 #pragma unroll
     for (int c = 0; c < kChunks; ++c) {
-      const int q = c * kThreads + (int)threadIdx.x;
+      const int q = c * kThreads + tid;
+      if (!owns(q)) continue;
       const int row = r0 + q / CPR, col = c0 + (q % CPR) * E;
       const T* p = g + (int64_t)row * ld + col;
       if (VEC && row < row_end && col + E <= col_end) {
@@ -122,10 +131,11 @@ struct Tile {
     }
   }
 
-  __device__ __forceinline__ void store(T* lds) const {
+  __device__ __forceinline__ void store(T* lds, int tid) const {
 #pragma unroll
     for (int c = 0; c < kChunks; ++c) {
-      const int q = c * kThreads + (int)threadIdx.x;
+      const int q = c * kThreads + tid;
+      if (!owns(q)) continue;
       u32x4_t w;
       __builtin_memcpy(&w, v[c], 16);
       *reinterpret_cast<u32x4_t*>(lds + (q / CPR) * PITCH + (q % CPR) * E) = w;
@@ -134,44 +144,53 @@ struct Tile {
 };
 
 // C[M][N] = A . B, A[m][k] at a[TA ? k*lda + m : m*lda + k], B[k][n] at
-// b[TB ? n*ldb + k : k*ldb + n].  Workgroup tile 128 x BN (BN = 128, or 64
-// when 128^2 tiles would leave CUs with a single workgroup); 4 waves of
-// 64 x BN/2.
-template <typename T, bool TA, bool TB, bool VEC, int BN, int BK, int OCC, bool VF, int BM = kBM>
-__global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restrict__ a, const T* __restrict__ b,
-                                                               T* __restrict__ c, int M, int N, int K, int64_t lda,
-                                                               int64_t ldb, int64_t ldc,
-                                                               const unsigned* __restrict__ gate, int splits_arg) {
-  // (the opt-in four-per-CU build has no register to spare for the atomic
-  // epilogue: no split-K there)
-  const int splits = OCC >= 4 ? 1 : splits_arg;
+// b[TB ? n*ldb + k : k*ldb + n].  Workgroup tile BM x BN (128 x 128, 128 x
+// 64, or for small products 64 x 64 / 64 x 32); 4 waves of BM/2 x BN/2 per K
+// group.
+//
+// KS = 2 (small products): two K groups of 4 waves each take one half of the
+// K tiles with their own LDS stages, and at the end group 1 hands its
+// accumulators to group 0 through LDS: C = fl(p0 + p1) in one fixed order, so
+// the product is deterministic with no C memset, no atomics and no
+// workspace.  (It replaces a two-way split over separate workgroups that
+// added both halves into a zeroed C with float atomics; that memset alone was
+// 5 us of a 36 us 1024^3 f32 product, profiles/r6_gemm_fp_trace.md.)
+//
+// RS register stages of global loads (RS = 2: three K tiles of loads in
+// flight), PIPE fragment lookahead (below).  su > 0 staggers the K loop:
+// workgroup b starts at K tile ((b % su) * ss) of its range and wraps (L2 /
+// HBM channel spread, rocBLAS's "StaggerU"; measured level here, so off by
+// default).  A group whose range ends in a partial K tile takes that tile
+// first instead, in the prologue, so every later load is a whole tile.  The
+// K order is fixed per output tile: the result is deterministic.
+template <typename T, bool TA, bool TB, bool VEC, int BM, int BN, int BK, int OCC, int KS, int RS, bool PIPE>
+__global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                                    T* __restrict__ c, int M, int N, int K,
+                                                                    int64_t lda, int64_t ldb, int64_t ldc,
+                                                                    const unsigned* __restrict__ gate, int su, int ss) {
   // gated launch (the split-bf16 f32 product's fallback, bk_gemm_f32x6):
   // runs only when the split found operands it cannot represent
   if (gate && *gate == 0) return;
   constexpr int PK = Cfg<T>::pitch_k(BK);
-  // BM = 64 (small products): each wave 32 rows -- MI 16-row blocks
-  constexpr int MI = BM / 32, kPitchM = BM + 16;
-  // vector fragment reads with a permuted k order (f32, BK % 16 == 0; f64's
-  // registers are too tight for the 2x fragment set); opt-in, BK_GEMM_FP_VEC=1
-  constexpr bool kVecFrag = std::is_same<T, float>::value && BK % 16 == 0 && VF;
+  constexpr int MI = BM / 32, kPitchM = BM + 16;  // MI 16-row blocks per wave
   constexpr int kPitchN = BN + 16;  // a [k][n] row: f64 = 32, f32 = 16 dwords mod 64 banks
   constexpr int WN = BN / 2, NT = WN / 16;  // wave columns, 16-wide MFMA tiles per wave row
+  static_assert(NT >= 1 && MI >= 1 && BK % 4 == 0, "tile");
   // A tile: [m][k] (row-major A) or [k][m] (A^T view); B tile: [k][n] or [n][k]
   using TileA = typename std::conditional<TA, Tile<T, VEC, BK, BM, kPitchM>, Tile<T, VEC, BM, BK, PK>>::type;
   using TileB = typename std::conditional<TB, Tile<T, VEC, BN, BK, PK>, Tile<T, VEC, BK, BN, kPitchN>>::type;
-  __shared__ __attribute__((aligned(16))) T lds_a[2][TileA::kLdsElems];
-  __shared__ __attribute__((aligned(16))) T lds_b[2][TileB::kLdsElems];
+  // LDS: per K group two stages of (A tile, B tile); KS = 2 reuses it for the
+  // hand-over of group 1's accumulators (4 waves x MI x NT x 4 x 64 values)
+  constexpr int kStage = TileA::kLdsElems + TileB::kLdsElems;
+  constexpr int kXchg = KS > 1 ? 4 * MI * NT * 4 * 64 : 0;
+  constexpr int kSmem = KS * 2 * kStage > kXchg ? KS * 2 * kStage : kXchg;
+  __shared__ __attribute__((aligned(16))) T smem[kSmem];
 
   // ---- tile of this block (XCD-aware, grouped) ----
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const int total = tiles_m * tiles_n;
-  int bid = (int)blockIdx.x;
-  // split-K (splits == 2, small grids): blocks [total, 2 total) take the
-  // second half of the K tiles and both halves add into a zeroed C -- two
-  // atomic adds onto 0 give fl(p0 + p1) in either order, so the result is
-  // deterministic (three or more would not be)
-  const int half = splits > 1 && bid >= total ? 1 : 0;
-  bid -= half * total;
+  const int raw = (int)blockIdx.x;
+  int bid = raw;
   if (total % kNumXCD == 0) bid = (bid % kNumXCD) * (total / kNumXCD) + bid / kNumXCD;
   constexpr int kGroup = 8;
   const int per_group = kGroup * tiles_n;
@@ -181,7 +200,9 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
   const int m0 = tm * BM, n0 = tn * BN;
   const bool interior = VEC && m0 + BM <= M && n0 + BN <= N;  // (uniform)
 
-  const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+  const int grp = KS > 1 ? (int)threadIdx.x / kThreads : 0;  // K group (wave-uniform)
+  const int tid = (int)threadIdx.x % kThreads;
+  const int lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * WN;
   const int fr = lane & 15, fk = lane >> 4;  // fragment: row/col within 16, k within 4
 
@@ -191,115 +212,190 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = acc_t<T>{0, 0, 0, 0};
 
-  TileA ta;
-  TileB tb;
-  auto load = [&](int k0) {
+  TileA ta[RS];
+  TileB tb[RS];
+  auto load_fast = [&](auto slot, int k0) {
+    constexpr int q = decltype(slot)::value;
+    if constexpr (TA)
+      ta[q].load_fast(a, lda, k0, m0, tid);
+    else
+      ta[q].load_fast(a, lda, m0, k0, tid);
+    if constexpr (TB)
+      tb[q].load_fast(b, ldb, n0, k0, tid);
+    else
+      tb[q].load_fast(b, ldb, k0, n0, tid);
+  };
+  auto load = [&](auto slot, int k0) {
+    constexpr int q = decltype(slot)::value;
     if (interior && k0 + BK <= K) {
-      if constexpr (TA)
-        ta.load_fast(a, lda, k0, m0);
-      else
-        ta.load_fast(a, lda, m0, k0);
-      if constexpr (TB)
-        tb.load_fast(b, ldb, n0, k0);
-      else
-        tb.load_fast(b, ldb, k0, n0);
+      load_fast(slot, k0);
     } else {
       if constexpr (TA)
-        ta.load_guarded(a, lda, K, M, k0, m0);
+        ta[q].load_guarded(a, lda, K, M, k0, m0, tid);
       else
-        ta.load_guarded(a, lda, M, K, m0, k0);
+        ta[q].load_guarded(a, lda, M, K, m0, k0, tid);
       if constexpr (TB)
-        tb.load_guarded(b, ldb, N, K, n0, k0);
+        tb[q].load_guarded(b, ldb, N, K, n0, k0, tid);
       else
-        tb.load_guarded(b, ldb, K, N, k0, n0);
+        tb[q].load_guarded(b, ldb, K, N, k0, n0, tid);
     }
   };
+  T* const stage0 = smem + grp * 2 * kStage;
+  auto lds_a = [&](int st) { return stage0 + st * kStage; };
+  auto lds_b = [&](int st) { return stage0 + st * kStage + TileA::kLdsElems; };
 
-  // Pipeline (two LDS stages, one register stage, loads two K tiles ahead):
-  // iteration kt first stores tile kt+1 -- loaded during iteration kt-1 --
-  // into the other LDS stage (last read in iteration kt-1, before the
-  // barrier that ended it), then issues tile kt+2's global loads into the
-  // freed registers, then runs tile kt's MFMAs.  The loads get a whole
-  // iteration of MFMAs to land before the next iteration stores them, and
-  // the one barrier per tile orders both the stage's reads and its writes.
-  // (The one-ahead loop this replaced waited for its loads right before the
-  // barrier: rocprofv3 SQ_WAIT_ANY 18% of f32 wave cycles against
-  // torch.matmul's 3%, profiles/r5_gemm_fp_pmc.md.)
-  const int nk_all = (K + BK - 1) / BK, nk_first = splits > 1 ? (nk_all + 1) / 2 : nk_all;
-  const int kt0 = half ? nk_first : 0;  // this block's K tiles: [kt0, kt0 + nk)
-  const int nk = half ? nk_all - nk_first : nk_first;
-  load(kt0 * BK);
-  ta.store(lds_a[0]);
-  tb.store(lds_b[0]);
-  if (nk > 1) load((kt0 + 1) * BK);
+  // Pipeline (two LDS stages, RS register stages, loads 1 + RS K tiles
+  // ahead): iteration kt first stores tile kt+1 -- in registers since
+  // iteration kt-RS -- into the other LDS stage (last read in iteration
+  // kt-1, before the barrier that ended it), then issues tile kt+1+RS's
+  // global loads into the freed registers, then runs tile kt's MFMAs.
+  const int nk_all = (K + BK - 1) / BK, nk_per = (nk_all + KS - 1) / KS;
+  const int kt0 = grp * nk_per;                      // this group's K tiles: [kt0, kt0 + nk)
+  const int nk = max(0, min(nk_per, nk_all - kt0));  // (group 1 may have one fewer, or none)
+  const bool partial = K % BK != 0 && kt0 + nk == nk_all;
+  const int rot = nk <= 0 ? 0 : partial ? nk - 1 : su > 0 ? (int)(((int64_t)(raw % su) * ss) % nk) : 0;
+  auto kpos = [&](int t) {  // K offset of this group's t-th tile
+    int r = t + rot;
+    if (r >= nk) r -= nk;
+    return (kt0 + r) * BK;
+  };
+  using S0 = std::integral_constant<int, 0>;
+  if (nk > 0) {
+    load(S0{}, kpos(0));
+    ta[0].store(lds_a(0), tid);
+    tb[0].store(lds_b(0), tid);
+    // tiles 1 .. RS into register slots t % RS
+    if (nk > 1) load(std::integral_constant<int, 1 % RS>{}, kpos(1));
+    if constexpr (RS > 1)
+      if (nk > 2) load(S0{}, kpos(2));
+  }
   __syncthreads();
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      ta.store(lds_a[cur ^ 1]);
-      tb.store(lds_b[cur ^ 1]);
-      if (kt + 2 < nk) load((kt0 + kt + 2) * BK);
+  // Fragment lookahead (PIPE): the fragments of MFMA step s+1 are read from
+  // LDS while step s's MFMAs run, and the next K tile's step 0 right after
+  // the iteration's one barrier, which sits before the last step's MFMAs.
+  // Without it every step read its fragments and waited for them
+  // (lgkmcnt(0)) before its MFMAs: f64 2048^3 waves spent 120K cycles in
+  // s_waitcnt against the Tensile kernel's 22K of the same 64 x 64 x 16 tile
+  // (profiles/r6_gemm_fp_pmc.md).
+  constexpr int kSteps = BK / 4;
+  T pa[MI], pb[NT];
+  auto read_frag = [&](const T* As, const T* Bs, int kk, T(&fa)[MI], T(&fb)[NT]) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = wm + i * 16 + fr, k = kk + fk;
+      fa[i] = TA ? As[k * kPitchM + m] : As[m * PK + k];
     }
-    const T* As = lds_a[cur];
-    const T* Bs = lds_b[cur];
-    if constexpr (kVecFrag) {
-      // f32: 16-B fragment reads.  The MFMA sums over k, so which k a lane
-      // contributes at which step is free as long as A and B agree: lane
-      // group g supplies k = kc + 4g + e at step e (of 4), so a lane's four
-      // A values for four steps are one ds_read_b128 of its [m][k] row (and
-      // B's too from an [n][k] view) instead of four ds_read_b32
 #pragma unroll
-      for (int kc = 0; kc < BK; kc += 16) {
-        f32x4 va[MI], vb[NT];
+    for (int j = 0; j < NT; ++j) {
+      const int n = wn + j * 16 + fr, k = kk + fk;
+      fb[j] = TB ? Bs[n * PK + k] : Bs[k * kPitchN + n];
+    }
+  };
+  if constexpr (PIPE)
+    if (nk > 0) read_frag(lds_a(0), lds_b(0), 0, pa, pb);
+
+  // An interior tile (`fast`) takes a branch-free variant: every iteration
+  // stores and loads (past the last tile it re-loads tile nk-1, a whole one,
+  // into a stage nobody reads), so the loads of the register slots stay in
+  // flight together -- with the guarded, branchy loads the compiler's wait
+  // before each LDS store drains every slot (vmcnt(0)).
+  const bool fast = (PIPE || RS > 1) && interior && nk == nk_per && (!partial || nk >= 2);
+  auto step = [&](int kt, auto slot, auto fast_tag) {  // slot = (kt + 1) % RS
+    constexpr int q = decltype(slot)::value;
+    constexpr bool kFast = decltype(fast_tag)::value;
+    const int cur = kt & 1;
+    if constexpr (kFast) {
+      ta[q].store(lds_a(cur ^ 1), tid);
+      tb[q].store(lds_b(cur ^ 1), tid);
+      load_fast(slot, kpos(min(kt + 1 + RS, nk - 1)));
+    } else {
+      if (kt >= nk) {  // (group 1's surplus iteration: only the barrier)
+        __syncthreads();
+        return;
+      }
+      if (kt + 1 < nk) {
+        ta[q].store(lds_a(cur ^ 1), tid);
+        tb[q].store(lds_b(cur ^ 1), tid);
+        if (kt + 1 + RS < nk) load(slot, kpos(kt + 1 + RS));
+      }
+    }
+    const T* As = lds_a(cur);
+    const T* Bs = lds_b(cur);
+    if constexpr (PIPE) {
 #pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const int m = wm + i * 16 + fr;
-          if constexpr (!TA) {
-            va[i] = *reinterpret_cast<const f32x4*>(&As[m * PK + kc + 4 * fk]);
-          } else {
+      for (int s4 = 0; s4 < kSteps; ++s4) {
+        T ca[MI], cb[NT];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) va[i][e] = As[(kc + 4 * fk + e) * kPitchM + m];
-          }
+        for (int i = 0; i < MI; ++i) ca[i] = pa[i];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) cb[j] = pb[j];
+        if (s4 + 1 < kSteps) {
+          read_frag(As, Bs, 4 * (s4 + 1), pa, pb);
+        } else {
+          // every wave stored tile kt+1 at the top of this iteration and
+          // issued its last reads of stage cur: the stages swap here
+          __syncthreads();
+          if (kFast || kt + 1 < nk) read_frag(lds_a(cur ^ 1), lds_b(cur ^ 1), 0, pa, pb);
         }
+        // (keeps the reads ahead of this step's MFMAs: the scheduler would
+        // sink them below, and the wait for them would then follow at once)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          const int n = wn + j * 16 + fr;
-          if constexpr (TB) {
-            vb[j] = *reinterpret_cast<const f32x4*>(&Bs[n * PK + kc + 4 * fk]);
-          } else {
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) vb[j][e] = Bs[(kc + 4 * fk + e) * kPitchN + n];
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NT; ++j) acc[i][j] = mfma((T)va[i][e], (T)vb[j][e], acc[i][j]);
+          for (int j = 0; j < NT; ++j) acc[i][j] = mfma(ca[i], cb[j], acc[i][j]);
       }
     } else {
+      // (the 128 x 128 tile: no registers for a lookahead set)
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 4) {
-      T fa[MI], fb[NT];
+      for (int kk = 0; kk < BK; kk += 4) {
+        T fa[MI], fb[NT];
+        read_frag(As, Bs, kk, fa, fb);
 #pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int m = wm + i * 16 + fr, k = kk + fk;
-        fa[i] = TA ? As[k * kPitchM + m] : As[m * PK + k];
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
       }
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int n = wn + j * 16 + fr, k = kk + fk;
-        fb[j] = TB ? Bs[n * PK + k] : Bs[k * kPitchN + n];
-      }
+      __syncthreads();
+    }
+  };
+  // (both variants run nk_per iterations: the K groups meet at every barrier)
+  auto run = [&](auto fast_tag) {
+    for (int kt = 0; kt < nk_per; kt += RS) {
+      step(kt, std::integral_constant<int, 1 % RS>{}, fast_tag);
+      if constexpr (RS > 1)
+        if (kt + 1 < nk_per) step(kt + 1, S0{}, fast_tag);
+    }
+  };
+  if (fast)
+    run(std::true_type{});
+  else
+    run(std::false_type{});
+
+  if constexpr (KS > 1) {
+    // group 1 -> LDS -> group 0 (the loop's last barrier ended every LDS read
+    // that counts; lookahead reads after it are discarded);
+    // value (i, j, r) of lane l of wave w at ((((w * MI + i) * NT + j) * 4 + r) * 64 + l):
+    // each store / load instruction covers 64 consecutive values
+    __syncthreads();
+    T* x = smem + (int64_t)wave * (MI * NT * 4 * 64) + lane;
+    if (grp == 1) {
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = mfma(fa[i], fb[j], acc[i][j]);
-    }
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x[((i * NT + j) * 4 + r) * 64] = acc[i][j][r];
     }
     __syncthreads();
+    if (grp == 1) return;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += x[((i * NT + j) * 4 + r) * 64];
   }
 
   // ---- epilogue: lanes 0..15 of a row are 16 consecutive columns ----
@@ -313,12 +409,7 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int n = n0 + wn + j * 16 + fr;
-        if (n < N) {
-          if (splits > 1)
-            unsafeAtomicAdd(crow + n, (T)acc[i][j][r]);  // (hardware float add; C was zeroed)
-          else
-            crow[n] = acc[i][j][r];
-        }
+        if (n < N) crow[n] = acc[i][j][r];
       }
     }
   }
@@ -330,7 +421,6 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_fp_kernel(const T* __restr
 // tile's time.  4000 x 3000 f64 at 2 per CU: 768 square tiles = 1.5 rounds
 // (0.75 of the slots busy) vs 1504 narrow ones = 2.94 (0.98): 66% -> 74% of
 // torch.matmul (profiles/archive/r5_gemm_fp_bench.jsonl, r5_gemm_fp_tiles.jsonl).
-// Small products (fewer square tiles than two per CU) always go narrow.
 inline double round_fill(int64_t tiles, int64_t slots) {
   const int64_t rounds = (tiles + slots - 1) / slots;
   return rounds > 0 ? (double)tiles / (double)(rounds * slots) : 1.0;
@@ -347,100 +437,109 @@ inline bool narrow_tiles(int M, int N, int occ) {
   return round_fill(tm * ((N + 63) / 64), slots) > round_fill(t128, slots) + 0.05;
 }
 
-// Tile shape and depth.  BK_GEMM_FP_BN (64 | 128) and BK_GEMM_FP_BK (a K
-// depth in elements) override the choice for A/B runs (tools/gemm_fp_bench.py).
+struct LaunchArgs {
+  const void *A, *B;
+  void* C;
+  int M, N, K;
+  int64_t lda, ldb, ldc;
+  hipStream_t stream;
+  const unsigned* gate;
+  int su, ss;
+  unsigned grid;
+};
+
+template <typename T, bool TA, bool TB, bool V, int BM, int BN, int BK, int OCC, int KS, int RS, bool PIPE>
+void go(const LaunchArgs& g) {
+  gemm_fp_kernel<T, TA, TB, V, BM, BN, BK, OCC, KS, RS, PIPE><<<g.grid, kThreads * KS, 0, g.stream>>>(
+      (const T*)g.A, (const T*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, g.gate, g.su, g.ss);
+}
+
+struct Shape {
+  int bm, bn, ks, rs;
+};
+
+// 64-row tiles (64 or 32 wide, one or two K groups) or 128-row ones (64 or
+// 128 wide); two register stages and the fragment lookahead everywhere but
+// the 128 x 128 tile, whose registers have no room for either (f64: 241
+// VGPRs of 256; f32 at three per CU: spills past 168)
+template <typename T, bool TA, bool TB, bool V, int BK, int OCC>
+void by_shape(const LaunchArgs& g, const Shape& s) {
+  constexpr bool kF64 = std::is_same<T, double>::value;
+  if (s.bm == 64) {
+    if (s.bn == 32)
+      s.rs == 2 ? go<T, TA, TB, V, 64, 32, BK, OCC, 1, 2, true>(g) : go<T, TA, TB, V, 64, 32, BK, OCC, 1, 1, true>(g);
+    else if (s.ks == 2)
+      s.rs == 2 ? go<T, TA, TB, V, 64, 64, BK, OCC, 2, 2, true>(g) : go<T, TA, TB, V, 64, 64, BK, OCC, 2, 1, true>(g);
+    else
+      s.rs == 2 ? go<T, TA, TB, V, 64, 64, BK, OCC, 1, 2, true>(g) : go<T, TA, TB, V, 64, 64, BK, OCC, 1, 1, true>(g);
+  } else if (s.bn == 64) {
+    s.rs == 2 ? go<T, TA, TB, V, 128, 64, BK, OCC, 1, 2, true>(g) : go<T, TA, TB, V, 128, 64, BK, OCC, 1, 1, true>(g);
+  } else {
+    go<T, TA, TB, V, 128, 128, BK, OCC, 1, 1, false>(g);
+  }
+}
+
+// Tile shape and depth (profiles/r6_gemm_fp_sweep.md).  For A/B runs
+// (tools/gemm_fp_bench.py, tools/gemm_fp_sweep.sh) the choice can be
+// overridden: BK_GEMM_FP_BN (32 | 64 | 128 columns), BK_GEMM_FP_BM (64 | 128
+// rows), BK_GEMM_FP_KS (1 | 2 K groups), BK_GEMM_FP_RS (1 | 2 register
+// stages), BK_GEMM_FP_BK (f32: 16 | 32 deep), BK_GEMM_FP_SU / _SS (stagger).
 template <typename T, bool TA, bool TB>
 void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, bool vec,
             hipStream_t stream, const unsigned* gate = nullptr) {
-  const char* ebn = getenv("BK_GEMM_FP_BN");
-  const char* ebk = getenv("BK_GEMM_FP_BK");
+  constexpr bool kF64 = std::is_same<T, double>::value;
+  auto env = [](const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+  };
   // f32: a 64-byte K tile (16 deep) halves the LDS a workgroup holds, so a
   // CU keeps three of them resident (its registers allow it) instead of two
-  const int bk_default = std::is_same<T, float>::value ? 16 : Cfg<T>::kDefaultBK;
-  const int bk = ebk ? atoi(ebk) : bk_default;
-  // f32 at 16 deep: three workgroups per CU.  Four fit too (<= 128 VGPRs,
-  // 38 KiB of LDS each; not A . B^T, whose [n][k] B reads then spill), but
-  // measured level with three: 4096^3 0.884 vs 0.885 of torch.matmul, 8192^3
-  // 0.881 both (profiles/archive/r5_gemm_fp_occ.jsonl) -- the waves' fragment-read
-  // waits after each barrier, not the slot count, hold it.  BK_GEMM_FP_OCC=4.
-  const char* eocc = getenv("BK_GEMM_FP_OCC");
-  constexpr bool kOcc4 = !(!TA && TB);
-  const int occ = std::is_same<T, float>::value && bk == 16 ? (kOcc4 && eocc && atoi(eocc) == 4 ? 4 : 3) : 2;
-  const bool nar = ebn ? atoi(ebn) == 64 : narrow_tiles(M, N, occ);
-  const int bn = nar ? 64 : 128;
-  // 64 x 64 tiles: f64 wherever 64-wide tiles were chosen, f32 when 128 x 64
-  // ones would give the CUs fewer than two workgroups each (1024^3: 128
-  // tiles).  The small kernel holds 84-99 VGPRs and 38 KiB of LDS (f64; f32
-  // 43-53 and 20 KiB), so a CU runs four or more of its workgroups at once:
-  // f64 1536^3 227 -> 179 us, 3072^3 1074 -> 934, 4000x3000x1000 495 -> 427
-  // (f32 at 2048^3 / 3072^3: level or slower; f64 4096^3 / 8192^3 with
-  // square tiles stay ahead of 64 x 64 ones, 2083 vs 2174 us;
-  // profiles/archive/r5_gemm_fp_bm64.jsonl).  BK_GEMM_FP_BM=128 turns it off, =64 on
-  // wherever the tiles are 64 wide (A/B runs).
-  const char* ebm = getenv("BK_GEMM_FP_BM");
-  const int64_t tiles_n = (N + bn - 1) / bn;
-  const bool small = nar && occ < 4 &&
-                     (ebm ? atoi(ebm) == 64
-                          : std::is_same<T, double>::value || ((M + kBM - 1) / kBM) * tiles_n < 2 * kNumCU);
-  const int bm = small ? 64 : kBM;
-  const int64_t tiles = (int64_t)((M + bm - 1) / bm) * tiles_n;
-  // split-K in two when the tiles fill at most half the chip's workgroup
-  // slots and each half keeps >= 8 K tiles (1024^3 f32: 128 tiles on 768
-  // slots); not for the gated fallback, whose C the split product wrote.
-  // BK_GEMM_FP_SPLITK=0 turns it off.
-  const char* esk = getenv("BK_GEMM_FP_SPLITK");
-  const int splits = !gate && occ < 4 && !(esk && atoi(esk) == 0) && 2 * tiles <= (int64_t)occ * kNumCU &&
-                             (K + bk - 1) / bk >= 16
-                         ? 2
-                         : 1;
-  if (splits > 1) {  // both halves add into C
-    const size_t row = (size_t)N * sizeof(T);
-    const hipError_t e = ldc == N ? hipMemsetAsync(C, 0, row * (size_t)M, stream)
-                                  : hipMemset2DAsync(C, (size_t)ldc * sizeof(T), 0, row, (size_t)M, stream);
-    if (e != hipSuccess) return;
-  }
-  const unsigned grid = (unsigned)(tiles * splits);
-  // vector fragment reads (BK_GEMM_FP_VEC=1): measured no faster on MI355X
-  // (4096^3 f32 126.7 vs 132.1 TFLOP/s, 8192^3 134.4 vs 135.0; their 5 more
-  // VGPRs cost a wave per SIMD), so the plain reads are the default
-  const bool vf = getenv("BK_GEMM_FP_VEC") && atoi(getenv("BK_GEMM_FP_VEC")) != 0;
-#define BK_FP_LAUNCH(V, W, D, O)                                                                              \
-  do {                                                                                                        \
-    if (small && (W) == 64 && (O) < 4) /* (plain fragment reads) */                                          \
-      gemm_fp_kernel<T, TA, TB, V, W, D, O, false, 64><<<grid, kThreads, 0, stream>>>(                           \
-          (const T*)A, (const T*)B, (T*)C, M, N, K, lda, ldb, ldc, gate, splits);                                 \
-    else if (vf && std::is_same<T, float>::value && (O) < 4) /* (at four per CU the vector reads spill) */     \
-      gemm_fp_kernel<T, TA, TB, V, W, D, O, std::is_same<T, float>::value && (O) < 4><<<grid, kThreads, 0,       \
-                                                                                     stream>>>(                \
-          (const T*)A, (const T*)B, (T*)C, M, N, K, lda, ldb, ldc, gate, splits);                                             \
-    else                                                                                                      \
-      gemm_fp_kernel<T, TA, TB, V, W, D, O, false><<<grid, kThreads, 0, stream>>>((const T*)A, (const T*)B,     \
-                                                                                 (T*)C, M, N, K, lda, ldb, ldc, gate, splits); \
-  } while (0)
-#define BK_FP_DEPTH(D, O)          \
-  do {                             \
-    if (vec && nar)                \
-      BK_FP_LAUNCH(true, 64, D, O);  \
-    else if (vec)                  \
-      BK_FP_LAUNCH(true, 128, D, O); \
-    else if (nar)                  \
-      BK_FP_LAUNCH(false, 64, D, O); \
-    else                           \
-      BK_FP_LAUNCH(false, 128, D, O); \
-  } while (0)
-  if constexpr (std::is_same<T, float>::value) {
-    constexpr int kHigh = kOcc4 ? 4 : 3;
-    if (kOcc4 && bk == 16 && occ == 4)
-      BK_FP_DEPTH(16, kHigh);
-    else if (bk == 16)
-      BK_FP_DEPTH(16, 3);
-    else
-      BK_FP_DEPTH(32, 2);
+  const int bk = kF64 ? 16 : (env("BK_GEMM_FP_BK", 16) == 32 ? 32 : 16);
+  const int occ = !kF64 && bk == 16 ? 3 : 2;
+  const int nk = (K + bk - 1) / bk;
+  // 64-row tiles while the 128-row ones would leave the CUs short of work:
+  //  * at most ~1.5 64 x 64 tiles per CU: two K groups per workgroup
+  //    (1024^3: 256 tiles; f64 47 vs 51 us with one group);
+  //  * fewer 64 x 64 tiles than the chip's ~3 slots per CU: 64 x 32 tiles
+  //    (1536^3: f64 151 vs 165 us, f32 84 vs 86);
+  //  * f64 wherever 128 x 128 tiles would not give every CU two (its
+  //    64 x 64 kernel runs three or four workgroups per CU: 2048^3 273 vs
+  //    ~300 us, 3072^3 856 vs 933); f32 while 128 x 64 tiles would not.
+  const int64_t t64 = (int64_t)((M + 63) / 64) * ((N + 63) / 64);
+  const int64_t slots = 3 * (int64_t)kNumCU;
+  Shape s{kBM, 128, 1, 2};
+  if (2 * t64 <= slots && nk >= 16) {
+    s = {64, 64, 2, 2};
+  } else if (t64 < slots) {
+    s = {64, 32, 1, 2};
   } else {
-    BK_FP_DEPTH(16, 2);
+    const bool nar = narrow_tiles(M, N, occ);
+    const bool small = nar && (kF64 || ((M + kBM - 1) / kBM) * (int64_t)((N + 63) / 64) < 2 * kNumCU);
+    s = {small ? 64 : kBM, nar ? 64 : 128, 1, 2};
   }
-#undef BK_FP_DEPTH
-#undef BK_FP_LAUNCH
+  s.bm = env("BK_GEMM_FP_BM", s.bm) == 64 ? 64 : kBM;
+  s.bn = env("BK_GEMM_FP_BN", s.bn);
+  if (s.bn != 32 && s.bn != 64) s.bn = 128;
+  if (s.bm == 64 && s.bn == 128) s.bn = 64;  // (64-row tiles come 64 or 32 wide)
+  if (s.bm == kBM && s.bn == 32) s.bn = 64;  // (and 128-row ones 64 or 128)
+  s.ks = s.bm == 64 && s.bn == 64 && env("BK_GEMM_FP_KS", s.ks) == 2 ? 2 : 1;
+  s.rs = env("BK_GEMM_FP_RS", s.rs) == 1 ? 1 : 2;
+  const int64_t tiles = (int64_t)((M + s.bm - 1) / s.bm) * ((N + s.bn - 1) / s.bn);
+  LaunchArgs g{A, B, C, M, N, K, lda, ldb, ldc, stream, gate, env("BK_GEMM_FP_SU", 0), env("BK_GEMM_FP_SS", 1),
+               (unsigned)tiles};
+  auto depth = [&](auto v) {
+    constexpr bool V = decltype(v)::value;
+    if constexpr (kF64)
+      by_shape<T, TA, TB, V, 16, 2>(g, s);
+    else if (bk == 16)
+      by_shape<T, TA, TB, V, 16, 3>(g, s);
+    else
+      by_shape<T, TA, TB, V, 32, 2>(g, s);
+  };
+  if (vec)
+    depth(std::true_type{});
+  else
+    depth(std::false_type{});
 }
 
 template <typename T>
@@ -591,8 +690,8 @@ BK_API int bk_gemm_fp(int dtype, int trans_a, int trans_b, const void* A, const 
   if (dtype != kF64 && dtype != kF32) return kBadArgument;
   if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0) return kBadArgument;
   if (lda < (trans_a ? M : K) || ldb < (trans_b ? K : N) || ldc < N) return kBadArgument;
-  const int64_t tiles = (int64_t)((M + 63) / 64) * ((N + 63) / 64);  // (the smallest tiles: 64 x 64)
-  if (2 * tiles > 0x7fffffffll) return kBadArgument;  // (split-K doubles the grid)
+  const int64_t tiles = (int64_t)((M + 63) / 64) * ((N + 31) / 32);  // (the smallest tiles: 64 x 32)
+  if (tiles > 0x7fffffffll) return kBadArgument;
   const int es = dtype_size(dtype);
   const int e = 16 / es;
   const bool vec = ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0) && lda % e == 0 && ldb % e == 0;

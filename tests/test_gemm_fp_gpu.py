@@ -177,9 +177,10 @@ def test_large_f32_matmul_routes_to_the_split_and_keeps_f32_precision(gpu):
 
 @pytest.mark.parametrize("dtype", ["float64", "float32"])
 def test_gemm_fp_split_k_is_deterministic_and_keeps_c_gaps(gpu, dtype):
-    """Small products split K in two (both halves add into a zeroed C): the
-    result is bitwise the same on every repeat, within the dtype's bound, and
-    a C with ldc > N keeps the columns past N untouched."""
+    """Small products split K over two wave groups of one workgroup (group 1
+    hands its half to group 0 through LDS): the result is bitwise the same on
+    every repeat, within the dtype's bound, and a C with ldc > N keeps the
+    columns past N untouched (no memset of C)."""
     from bee_code_interpreter_fs_amd.ops import _native
     from bee_code_interpreter_fs_amd.ops.array import DeviceArray, driver
 

@@ -131,7 +131,7 @@ def test_matmul_of_f64_arrays_runs_at_numpy_precision(drv, monkeypatch):
 
 
 def test_large_f32_matmul_takes_the_split_bf16_product(drv, monkeypatch):
-    """f32 products from 2^32 multiply-adds (M, N >= 256) run as the six-piece
+    """f32 products above 2^33 multiply-adds (M, N >= 256) run as the six-piece
     bf16 split (gemm_f32x6) with an exactly-sized workspace; small ones, f64,
     BEE_GEMM_F32X6=0 and a quota with no room for the workspace stay on the
     f32 / f64 MFMA (gemm_fp)."""
@@ -139,18 +139,18 @@ def test_large_f32_matmul_takes_the_split_bf16_product(drv, monkeypatch):
 
     arr = importlib.import_module("bee_code_interpreter_fs_amd.ops.array")  # (ops.array is the function)
     rng = np.random.default_rng(5)
-    a_h = rng.standard_normal((2048, 1024)).astype(np.float32)
-    b_h = rng.standard_normal((2048, 1024)).astype(np.float32)
+    a_h = rng.standard_normal((2048, 2560)).astype(np.float32)
+    b_h = rng.standard_normal((2048, 2560)).astype(np.float32)
     a, b = ops.asarray(a_h), ops.asarray(b_h)
     drv.launches.clear()
-    c = np.matmul(a, b.T)  # 2048 x 2048 x 1024 = 2^32
+    c = np.matmul(a, b.T)  # 2048 x 2048 x 2560 > 2^33
     assert kernels(drv) == ["gemm_f32x6"] and drv.launches[0][-2:] == (False, True), drv.launches
     assert c.dtype == "float32"
     np.testing.assert_allclose(c.numpy(), a_h @ b_h.T, rtol=1e-4, atol=1e-3)
     assert arr.f32x6_workspace_bytes(1024, 1024, 1000) == 256 + 12 * 1024 * 2048
     drv.launches.clear()
     np.matmul(ops.asarray(a_h[:200]), b.T)  # M < 256
-    np.matmul(ops.asarray(a_h[:, :1000]), ops.asarray(b_h[:, :1000].T))  # below 2^32
+    np.matmul(ops.asarray(a_h[:, :2048]), ops.asarray(b_h[:, :2048].T))  # 2^33: not above
     np.matmul(ops.asarray(a_h.astype(np.float64)), ops.asarray(b_h.T.astype(np.float64)))
     monkeypatch.setattr(arr, "_F32X6", "0")
     np.matmul(a, b.T)
@@ -160,7 +160,7 @@ def test_large_f32_matmul_takes_the_split_bf16_product(drv, monkeypatch):
     real_malloc = drv.malloc
 
     def tight(nbytes):  # the workspace does not fit the quota
-        if nbytes >= arr.f32x6_workspace_bytes(2048, 2048, 1024):
+        if nbytes >= arr.f32x6_workspace_bytes(2048, 2048, 2560):
             raise ops.QuotaExceeded("no room")
         return real_malloc(nbytes)
 

@@ -35,25 +35,32 @@ def load(d):
 
 def main():
     root, dt, n = sys.argv[1], sys.argv[2], int(sys.argv[3])
-    print(f"| impl | kernel | us | GHz | wave cyc | busy | wait_any | wait_inst | wait_lds | MFMA busy | VALU insts/wave | LDS insts/wave |")
-    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
-    for impl in ("bk", "torch"):
+    impls = sys.argv[4:] or ["bk", "torch"]
+    print("| impl | kernel | us | GHz | wave cyc | busy | wait_any | wait_inst | wait_lds | MFMA busy | VALU insts/wave "
+          "| LDS insts/wave | LDS bank-conflict / active | VMEM insts/wave |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
+    for impl in impls:
         v, dur = {}, None
-        for p in (1, 2):
-            a, d = load(os.path.join(root, f"pmc_{dt}_{n}_{impl}_{p}"))
+        for p in (1, 2, 3):
+            d = os.path.join(root, f"pmc_{dt}_{n}_{impl}_{p}")
+            if not os.path.isdir(d):
+                continue
+            a, du = load(d)
             v.update(a)
-            dur = dur or d
+            dur = dur or du
         if not v or not dur:
             print(f"| {impl} | (no data) |")
             continue
         waves = v.get("SQ_WAVES", 1)
-        q = lambda c: v.get(c, float("nan")) * 4 / waves  # noqa: E731  (quad-cycles -> cycles per wave)
+        nan = float("nan")
+        q = lambda c: v.get(c, nan) * 4 / waves  # noqa: E731  (quad-cycles -> cycles per wave)
         clk = v["GRBM_GUI_ACTIVE"] / 8
-        busy = v.get("SQ_VALU_MFMA_BUSY_CYCLES", float("nan")) / (clk * 256 * 4)
+        busy = v.get("SQ_VALU_MFMA_BUSY_CYCLES", nan) / (clk * 256 * 4)
+        conf = v.get("SQ_LDS_BANK_CONFLICT", nan) / v.get("SQ_LDS_IDX_ACTIVE", nan)
         print(f"| {impl} | {v['_kernel'][:48]} | {dur / 1e3:.1f} | {clk / dur:.2f} | {q('SQ_WAVE_CYCLES'):.0f} | "
               f"{q('SQ_BUSY_CYCLES'):.0f} | {q('SQ_WAIT_ANY'):.0f} | {q('SQ_WAIT_INST_ANY'):.0f} | "
-              f"{q('SQ_WAIT_INST_LDS'):.0f} | {busy:.3f} | {v.get('SQ_INSTS_VALU', float('nan')) / waves:.0f} | "
-              f"{v.get('SQ_INSTS_LDS', float('nan')) / waves:.0f} |")
+              f"{q('SQ_WAIT_INST_LDS'):.0f} | {busy:.3f} | {v.get('SQ_INSTS_VALU', nan) / waves:.0f} | "
+              f"{v.get('SQ_INSTS_LDS', nan) / waves:.0f} | {conf:.3f} | {v.get('SQ_INSTS_VMEM', nan) / waves:.0f} |")
 
 
 if __name__ == "__main__":

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 6, session 11: fragment lookahead in the 64-row f64 / f32 GEMM tiles
+# -- tests, counters at f64 2048^3, the RS / KS sweep.
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+source tools/gpu_steps.sh
+rm -f gpurun_out/gemm_fp_sweep.jsonl
+rm -rf gpurun_out/pmc_*
+step fp_tests 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gemm_fp_gpu.py
+grep -q "passed" gpurun_out/fp_tests.log && ! grep -q "failed\|error" gpurun_out/fp_tests.log || { echo "tests failed"; exit 1; }
+IMPLS=bk PASSES="1 2 3" step pmc_a 300 bash tools/gemm_fp_pmc.sh float64 2048
+BK_GEMM_FP_RS=2 IMPLS=bk TAG=rs2 PASSES="1 2 3" step pmc_b 300 bash tools/gemm_fp_pmc.sh float64 2048
+SIZES="1024 1536 2048 3072" step fp_sweep 900 bash tools/gemm_fp_sweep.sh "la" "la_rs2 BK_GEMM_FP_RS=2" "la_rs2ks1 BK_GEMM_FP_RS=2 BK_GEMM_FP_KS=1" "la_bn32 BK_GEMM_FP_BN=32 BK_GEMM_FP_KS=1 BK_GEMM_FP_RS=2"
