@@ -49,7 +49,11 @@ constexpr int kBM = 128, kBN = 128, kThreads = 256;
 constexpr int kPitchMN = 128 + 16;  // LDS row of an [k][m|n] tile: 144 elements
 
 // K tile: 128 B per row by default (16 f64 / 32 f32); an [m|n][k] LDS row is
-// padded by 16 B so a fragment read (16 rows x 4 k) hits 64 distinct banks
+// padded by 16 B.  (Padding f32 rows by 8 B instead -- conflict-free for the
+// ds_read_b32 banking, (a/4) mod 32 -- and keeping every fragment read a
+// single ds_read_b32 / _b64 rather than the compiler's ds_read2 pairs measured
+// slower everywhere: 2048^3 f32 164 vs 143 us, f64 303 vs 277; the pairs
+// halve the LDS instructions and their address arithmetic.)
 template <typename T>
 struct Cfg {
   static constexpr int kDefaultBK = 128 / sizeof(T);
@@ -136,9 +140,17 @@ struct Tile {
     for (int c = 0; c < kChunks; ++c) {
       const int q = c * kThreads + tid;
       if (!owns(q)) continue;
-      u32x4_t w;
-      __builtin_memcpy(&w, v[c], 16);
-      *reinterpret_cast<u32x4_t*>(lds + (q / CPR) * PITCH + (q % CPR) * E) = w;
+      T* dst = lds + (q / CPR) * PITCH + (q % CPR) * E;
+      if constexpr (PITCH * sizeof(T) % 16 == 0) {
+        u32x4_t w;
+        __builtin_memcpy(&w, v[c], 16);
+        *reinterpret_cast<u32x4_t*>(dst) = w;
+      } else {  // (8-B aligned rows)
+        uint64_t w[2];
+        __builtin_memcpy(w, v[c], 16);
+        reinterpret_cast<uint64_t*>(dst)[0] = w[0];
+        reinterpret_cast<uint64_t*>(dst)[1] = w[1];
+      }
     }
   }
 };
@@ -190,8 +202,11 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const int total = tiles_m * tiles_n;
   const int raw = (int)blockIdx.x;
-  int bid = raw;
-  if (total % kNumXCD == 0) bid = (bid % kNumXCD) * (total / kNumXCD) + bid / kNumXCD;
+  // XCD-aware order: blocks are dealt round-robin over the 8 XCDs, so XCD x
+  // runs blocks x, x+8, ...; they get a contiguous range of tiles (the first
+  // total % 8 XCDs one more), whose A / B panels then share that XCD's L2
+  const int per_xcd = total / kNumXCD, extra = total % kNumXCD, xcd = raw % kNumXCD;
+  const int bid = xcd * per_xcd + min(xcd, extra) + raw / kNumXCD;
   constexpr int kGroup = 8;
   const int per_group = kGroup * tiles_n;
   const int first_m = (bid / per_group) * kGroup;
@@ -472,10 +487,11 @@ void by_shape(const LaunchArgs& g, const Shape& s) {
       s.rs == 2 ? go<T, TA, TB, V, 64, 64, BK, OCC, 2, 2, true>(g) : go<T, TA, TB, V, 64, 64, BK, OCC, 2, 1, true>(g);
     else
       s.rs == 2 ? go<T, TA, TB, V, 64, 64, BK, OCC, 1, 2, true>(g) : go<T, TA, TB, V, 64, 64, BK, OCC, 1, 1, true>(g);
-  } else if (s.bn == 64) {
-    s.rs == 2 ? go<T, TA, TB, V, 128, 64, BK, OCC, 1, 2, true>(g) : go<T, TA, TB, V, 128, 64, BK, OCC, 1, 1, true>(g);
-  } else {
-    go<T, TA, TB, V, 128, 128, BK, OCC, 1, 1, false>(g);
+  } else if constexpr (!(kF64 && BK == 32)) {  // (f64 32-deep: 64-row tiles only)
+    if (s.bn == 64)
+      s.rs == 2 ? go<T, TA, TB, V, 128, 64, BK, OCC, 1, 2, true>(g) : go<T, TA, TB, V, 128, 64, BK, OCC, 1, 1, true>(g);
+    else
+      go<T, TA, TB, V, 128, 128, BK, OCC, 1, 1, false>(g);
   }
 }
 
@@ -494,7 +510,7 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   };
   // f32: a 64-byte K tile (16 deep) halves the LDS a workgroup holds, so a
   // CU keeps three of them resident (its registers allow it) instead of two
-  const int bk = kF64 ? 16 : (env("BK_GEMM_FP_BK", 16) == 32 ? 32 : 16);
+  const int bk = env("BK_GEMM_FP_BK", 16) == 32 ? 32 : 16;
   const int occ = !kF64 && bk == 16 ? 3 : 2;
   const int nk = (K + bk - 1) / bk;
   // 64-row tiles while the 128-row ones would leave the CUs short of work:
@@ -502,9 +518,10 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   //    (1024^3: 256 tiles; f64 47 vs 51 us with one group);
   //  * fewer 64 x 64 tiles than the chip's ~3 slots per CU: 64 x 32 tiles
   //    (1536^3: f64 151 vs 165 us, f32 84 vs 86);
-  //  * f64 wherever 128 x 128 tiles would not give every CU two (its
-  //    64 x 64 kernel runs three or four workgroups per CU: 2048^3 273 vs
-  //    ~300 us, 3072^3 856 vs 933); f32 while 128 x 64 tiles would not.
+  //  * f64 everywhere else (its 64 x 64 kernel runs three workgroups per
+  //    CU: 3072^3 856 vs 933 us, 4096^3 2001 vs 2126 with 128 x 128 tiles,
+  //    8192^3 15952 vs 16661); f32 while 128 x 64 tiles would not give
+  //    every CU two.
   const int64_t t64 = (int64_t)((M + 63) / 64) * ((N + 63) / 64);
   const int64_t slots = 3 * (int64_t)kNumCU;
   Shape s{kBM, 128, 1, 2};
@@ -512,9 +529,11 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
     s = {64, 64, 2, 2};
   } else if (t64 < slots) {
     s = {64, 32, 1, 2};
+  } else if (kF64) {
+    s = {64, 64, 1, 2};
   } else {
     const bool nar = narrow_tiles(M, N, occ);
-    const bool small = nar && (kF64 || ((M + kBM - 1) / kBM) * (int64_t)((N + 63) / 64) < 2 * kNumCU);
+    const bool small = nar && ((M + kBM - 1) / kBM) * (int64_t)((N + 63) / 64) < 2 * kNumCU;
     s = {small ? 64 : kBM, nar ? 64 : 128, 1, 2};
   }
   s.bm = env("BK_GEMM_FP_BM", s.bm) == 64 ? 64 : kBM;
@@ -529,9 +548,12 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
                (unsigned)tiles};
   auto depth = [&](auto v) {
     constexpr bool V = decltype(v)::value;
-    if constexpr (kF64)
-      by_shape<T, TA, TB, V, 16, 2>(g, s);
-    else if (bk == 16)
+    if constexpr (kF64) {
+      if (bk == 32 && s.bm == 64)  // (A/B runs; 128-row f64 tiles have no registers for it)
+        by_shape<T, TA, TB, V, 32, 2>(g, s);
+      else
+        by_shape<T, TA, TB, V, 16, 2>(g, s);
+    } else if (bk == 16)
       by_shape<T, TA, TB, V, 16, 3>(g, s);
     else
       by_shape<T, TA, TB, V, 32, 2>(g, s);
