@@ -166,7 +166,7 @@ struct Tile {
 // the product is deterministic with no C memset, no atomics and no
 // workspace.  (It replaces a two-way split over separate workgroups that
 // added both halves into a zeroed C with float atomics; that memset alone was
-// 5 us of a 36 us 1024^3 f32 product, profiles/r6_gemm_fp_trace.md.)
+// 5 us of a 36 us 1024^3 f32 product, profiles/r6_gemm_fp_pmc.md.)
 //
 // RS register stages of global loads (RS = 2: three K tiles of loads in
 // flight), PIPE fragment lookahead (below).  su > 0 staggers the K loop:
@@ -495,7 +495,7 @@ void by_shape(const LaunchArgs& g, const Shape& s) {
   }
 }
 
-// Tile shape and depth (profiles/r6_gemm_fp_sweep.md).  For A/B runs
+// Tile shape and depth (profiles/r6_gemm_fp_sweep.jsonl).  For A/B runs
 // (tools/gemm_fp_bench.py, tools/gemm_fp_sweep.sh) the choice can be
 // overridden: BK_GEMM_FP_BN (32 | 64 | 128 columns), BK_GEMM_FP_BM (64 | 128
 // rows), BK_GEMM_FP_KS (1 | 2 K groups), BK_GEMM_FP_RS (1 | 2 register
