@@ -73,24 +73,33 @@ def test_gemm_fp_unaligned_leading_dimensions(gpu):
 @pytest.mark.parametrize("M,N,K,lda,ldb,ldc", [(130, 126, 34, 34, 126, 126), (70, 2, 18, 24, 4, 5),
                                                 (200, 136, 1000, 1002, 140, 137), (1, 64, 2, 2, 64, 64),
                                                 (64, 65, 4098, 4100, 66, 65), (3000, 40, 96, 96, 40, 40)])
-def test_gemm_f64_ragged_and_padded(gpu, M, N, K, lda, ldb, ldc):
-    """Row-major f64 on the 16-B load path: ragged M / N / K, K not a
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+def test_gemm_fp_ragged_and_padded(gpu, dtype, M, N, K, lda, ldb, ldc):
+    """Row-major f64 / f32 on the 16-B load path: ragged M / N / K, K not a
     multiple of the 16-deep tile (its partial tile goes first), sub-matrices
-    of wider buffers (lda > K, ldb > N) and ldc > N, against fp64; the columns
-    past N are left alone, and repeats are bitwise the same."""
+    of wider buffers (lda > K, ldb > N, NaN-filled past the edges) and
+    ldc > N, against fp64; the columns past N are left alone, and repeats are
+    bitwise the same."""
     from bee_code_interpreter_fs_amd.ops import _native
     from bee_code_interpreter_fs_amd.ops.array import DeviceArray, driver
 
     rng = np.random.default_rng(M + 3 * N + 7 * K)
+    # NaN wherever the product must not read: A's columns past K, B's
+    # columns past N and 16 rows past K (a tile read past the edge shows up
+    # as NaN in C)
     A = rng.standard_normal((M, lda))
-    B = rng.standard_normal((K, ldb))
+    A[:, K:] = np.nan
+    B = rng.standard_normal((K + 16, ldb))
+    B[K:, :] = np.nan
+    B[:, N:] = np.nan
+    A, B = A.astype(dtype), B.astype(dtype)
     a, b = gpu.asarray(A), gpu.asarray(B)
-    c = gpu.asarray(np.full((M, ldc), 7.0))
-    dt = _native.DTYPE_CODES["float64"]
+    c = gpu.asarray(np.full((M, ldc), 7.0, dtype=dtype))
+    dt = _native.DTYPE_CODES[dtype]
     driver().gemm_fp(dt, False, False, a.ptr, b.ptr, c.ptr, M, N, K, lda, ldb, ldc)
     first = c.numpy()
     assert (first[:, N:] == 7.0).all()
-    _check(first[:, :N], A[:, :K], B[:, :N], "float64")
+    _check(first[:, :N], A[:, :K].astype(np.float64), B[:K, :N].astype(np.float64), dtype)
     driver().gemm_fp(dt, False, False, a.ptr, b.ptr, c.ptr, M, N, K, lda, ldb, ldc)
     np.testing.assert_array_equal(c.numpy(), first)
     assert isinstance(c, DeviceArray)
