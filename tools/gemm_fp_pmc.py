@@ -39,9 +39,10 @@ def main():
     print("| impl | kernel | us | GHz | wave cyc | busy | wait_any | wait_inst | wait_lds | MFMA busy | VALU insts/wave "
           "| LDS insts/wave | LDS bank-conflict / active | VMEM insts/wave |")
     print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
+    mem = []
     for impl in impls:
         v, dur = {}, None
-        for p in (1, 2, 3):
+        for p in (1, 2, 3, 4):
             d = os.path.join(root, f"pmc_{dt}_{n}_{impl}_{p}")
             if not os.path.isdir(d):
                 continue
@@ -61,6 +62,18 @@ def main():
               f"{q('SQ_BUSY_CYCLES'):.0f} | {q('SQ_WAIT_ANY'):.0f} | {q('SQ_WAIT_INST_ANY'):.0f} | "
               f"{q('SQ_WAIT_INST_LDS'):.0f} | {busy:.3f} | {v.get('SQ_INSTS_VALU', nan) / waves:.0f} | "
               f"{v.get('SQ_INSTS_LDS', nan) / waves:.0f} | {conf:.3f} | {v.get('SQ_INSTS_VMEM', nan) / waves:.0f} |")
+        if "TCC_HIT_sum" in v:
+            hit = v["TCC_HIT_sum"] / max(1.0, v["TCC_HIT_sum"] + v.get("TCC_MISS_sum", 0))
+            lat = v.get("SQ_INST_LEVEL_VMEM", nan) / max(1.0, v.get("SQ_INSTS_VMEM_RD", nan))
+            mem.append(f"| {impl} | L2 hit {hit:.3f} | EA read req {v.get('TCC_EA0_RDREQ_sum', nan):.3e} | "
+                       f"VMEM level/read {lat:.1f} | TA busy {v.get('TA_BUSY_avr', nan):.3e} |")
+
+
+    if mem:
+        print()
+        print("| impl | L2 | HBM | VMEM latency (level / reads) | TA |")
+        print("|---|---|---|---|---|")
+        print("\n".join(mem))
 
 
 if __name__ == "__main__":
