@@ -116,6 +116,25 @@ struct Tile {
     }
   }
 
+  // Through a buffer descriptor whose range (num_records) ends the panel:
+  // rows past it read as zero, and so do chunks at or past column `col_lim`
+  // (their offset is moved out of range: the caller passes the K extent
+  // when the tile's columns run along K, so a partial K tile and the
+  // K tiles past the end are zeros).  No branches: every tile, edges
+  // included, loads the same way (BUF).  (r0, c0) are panel-relative.
+  __device__ __forceinline__ void load_buf(__amdgpu_buffer_rsrc_t rsrc, int64_t ld, int r0, int c0, int col_lim,
+                                           int tid) {
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) {
+      const int q = c * kThreads + tid;
+      if (!owns(q)) continue;
+      const int row = r0 + q / CPR, col = c0 + (q % CPR) * E;
+      const int off = col < col_lim ? (int)(((int64_t)row * ld + col) * (int64_t)sizeof(T)) : (int)0x80000000;
+      const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+      __builtin_memcpy(v[c], &x, 16);
+    }
+  }
+
   // edge tiles: out-of-range elements are zero
   __device__ __forceinline__ void load_guarded(const T* __restrict__ g, int64_t ld, int row_end, int col_end, int r0,
                                                int c0, int tid) {
@@ -175,7 +194,8 @@ struct Tile {
 // default).  A group whose range ends in a partial K tile takes that tile
 // first instead, in the prologue, so every later load is a whole tile.  The
 // K order is fixed per output tile: the result is deterministic.
-template <typename T, bool TA, bool TB, bool VEC, int BM, int BN, int BK, int OCC, int KS, int RS, bool PIPE>
+template <typename T, bool TA, bool TB, bool VEC, int BM, int BN, int BK, int OCC, int KS, int RS, bool PIPE,
+          bool BUF = false>
 __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __restrict__ a, const T* __restrict__ b,
                                                                     T* __restrict__ c, int M, int N, int K,
                                                                     int64_t lda, int64_t ldb, int64_t ldc,
@@ -240,9 +260,34 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
     else
       tb[q].load_fast(b, ldb, k0, n0, tid);
   };
+  // BUF: one buffer descriptor per operand panel -- A's rows m0.. ([m][k])
+  // or its columns m0.. over all K rows ([k][m]), B's columns n0.. over all K
+  // rows ([k][n]) or its rows n0.. ([n][k]) -- whose range ends at the
+  // matrix's last element, so rows past M / N / K read as zero
+  // (launch() checks every panel offset fits 31 bits)
+  auto panel = [](const T* base, int64_t elems) {
+    const int64_t bytes = elems * (int64_t)sizeof(T);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(bytes < 0 ? 0 : bytes), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t ra =
+      TA ? panel(a + m0, (int64_t)(K - 1) * lda + M - m0) : panel(a + (int64_t)m0 * lda, (int64_t)(M - m0 - 1) * lda + K);
+  const __amdgpu_buffer_rsrc_t rb =
+      TB ? panel(b + (int64_t)n0 * ldb, (int64_t)(N - n0 - 1) * ldb + K) : panel(b + n0, (int64_t)(K - 1) * ldb + N - n0);
+  constexpr int kNoLim = 0x7fffffff;
   auto load = [&](auto slot, int k0) {
     constexpr int q = decltype(slot)::value;
-    if (interior && k0 + BK <= K) {
+    if constexpr (BUF) {
+      // (columns past M / N of the [k][m] / [k][n] views read neighbours'
+      // values: they only feed C's rows / columns past the edge, never stored)
+      if constexpr (TA)
+        ta[q].load_buf(ra, lda, k0, 0, kNoLim, tid);
+      else
+        ta[q].load_buf(ra, lda, 0, k0, K, tid);
+      if constexpr (TB)
+        tb[q].load_buf(rb, ldb, 0, k0, K, tid);
+      else
+        tb[q].load_buf(rb, ldb, k0, 0, kNoLim, tid);
+    } else if (interior && k0 + BK <= K) {
       load_fast(slot, k0);
     } else {
       if constexpr (TA)
@@ -270,19 +315,20 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
   const bool partial = K % BK != 0 && kt0 + nk == nk_all;
   const int rot = nk <= 0 ? 0 : partial ? nk - 1 : su > 0 ? (int)(((int64_t)(raw % su) * ss) % nk) : 0;
   auto kpos = [&](int t) {  // K offset of this group's t-th tile
+    if (BUF && t >= nk) return nk_all * BK;  // (BUF: past the group's range, a tile of zeros)
     int r = t + rot;
     if (r >= nk) r -= nk;
     return (kt0 + r) * BK;
   };
   using S0 = std::integral_constant<int, 0>;
-  if (nk > 0) {
+  if (BUF || nk > 0) {
     load(S0{}, kpos(0));
     ta[0].store(lds_a(0), tid);
     tb[0].store(lds_b(0), tid);
     // tiles 1 .. RS into register slots t % RS
-    if (nk > 1) load(std::integral_constant<int, 1 % RS>{}, kpos(1));
+    if (BUF || nk > 1) load(std::integral_constant<int, 1 % RS>{}, kpos(1));
     if constexpr (RS > 1)
-      if (nk > 2) load(S0{}, kpos(2));
+      if (BUF || nk > 2) load(S0{}, kpos(2));
   }
   __syncthreads();
 
@@ -315,7 +361,7 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
   // into a stage nobody reads), so the loads of the register slots stay in
   // flight together -- with the guarded, branchy loads the compiler's wait
   // before each LDS store drains every slot (vmcnt(0)).
-  const bool fast = (PIPE || RS > 1) && interior && nk == nk_per && (!partial || nk >= 2);
+  const bool fast = BUF || ((PIPE || RS > 1) && interior && nk == nk_per && (!partial || nk >= 2));
   auto step = [&](int kt, auto slot, auto fast_tag) {  // slot = (kt + 1) % RS
     constexpr int q = decltype(slot)::value;
     constexpr bool kFast = decltype(fast_tag)::value;
@@ -323,7 +369,10 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
     if constexpr (kFast) {
       ta[q].store(lds_a(cur ^ 1), tid);
       tb[q].store(lds_b(cur ^ 1), tid);
-      load_fast(slot, kpos(min(kt + 1 + RS, nk - 1)));
+      if constexpr (BUF)
+        load(slot, kpos(kt + 1 + RS));  // (past the end: zero tiles)
+      else
+        load_fast(slot, kpos(min(kt + 1 + RS, nk - 1)));
     } else {
       if (kt >= nk) {  // (group 1's surplus iteration: only the barrier)
         __syncthreads();
@@ -383,10 +432,17 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
         if (kt + 1 < nk_per) step(kt + 1, S0{}, fast_tag);
     }
   };
-  if (fast)
+  // (BUF: one branch-free loop for every tile; the guarded variant and its
+  // registers are not in the kernel at all -- f64 64 x 64: 110 VGPRs
+  // against 152, a fourth workgroup per CU)
+  if constexpr (BUF) {
     run(std::true_type{});
-  else
-    run(std::false_type{});
+  } else {
+    if (fast)
+      run(std::true_type{});
+    else
+      run(std::false_type{});
+  }
 
   if constexpr (KS > 1) {
     // group 1 -> LDS -> group 0 (the loop's last barrier ended every LDS read
@@ -461,10 +517,18 @@ struct LaunchArgs {
   const unsigned* gate;
   int su, ss;
   unsigned grid;
+  bool buf;  // the branch-free buffer-load kernels (BUF) take this product
 };
 
 template <typename T, bool TA, bool TB, bool V, int BM, int BN, int BK, int OCC, int KS, int RS, bool PIPE>
 void go(const LaunchArgs& g) {
+  if constexpr (V) {
+    if (g.buf) {
+      gemm_fp_kernel<T, TA, TB, true, BM, BN, BK, OCC, KS, RS, PIPE, true><<<g.grid, kThreads * KS, 0, g.stream>>>(
+          (const T*)g.A, (const T*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, g.gate, g.su, g.ss);
+      return;
+    }
+  }
   gemm_fp_kernel<T, TA, TB, V, BM, BN, BK, OCC, KS, RS, PIPE><<<g.grid, kThreads * KS, 0, g.stream>>>(
       (const T*)g.A, (const T*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, g.gate, g.su, g.ss);
 }
@@ -544,8 +608,15 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   s.ks = s.bm == 64 && s.bn == 64 && env("BK_GEMM_FP_KS", s.ks) == 2 ? 2 : 1;
   s.rs = env("BK_GEMM_FP_RS", s.rs) == 1 ? 1 : 2;
   const int64_t tiles = (int64_t)((M + s.bm - 1) / s.bm) * ((N + s.bn - 1) / s.bn);
+  // BUF (branch-free buffer loads, the guarded path compiled out) when the
+  // 16-B chunks along K are all in or all out (K a multiple of the chunk)
+  // and every panel offset -- rows up to a tile past the edge -- fits 31 bits
+  constexpr int kE = 16 / (int)sizeof(T);
+  auto fits = [](int64_t rows, int64_t ld) { return (rows + 256) * ld * (int64_t)sizeof(T) < 0x7fffffffll; };
+  const bool buf = vec && K % kE == 0 && env("BK_GEMM_FP_BUF", 1) != 0 &&
+                   fits(TA ? K : s.bm, lda) && fits(TB ? s.bn : K, ldb);
   LaunchArgs g{A, B, C, M, N, K, lda, ldb, ldc, stream, gate, env("BK_GEMM_FP_SU", 0), env("BK_GEMM_FP_SS", 1),
-               (unsigned)tiles};
+               (unsigned)tiles, buf};
   auto depth = [&](auto v) {
     constexpr bool V = decltype(v)::value;
     if constexpr (kF64) {
