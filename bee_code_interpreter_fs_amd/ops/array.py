@@ -616,10 +616,10 @@ def _fp_dtype(x) -> bool:
 # bk_gemm_f32x6: f32-level error at the bf16 MFMA's rate) above 2^33
 # multiply-adds with M, N >= 256; smaller ones, and any product whose
 # workspace the HBM quota refuses, run on the f32 MFMA.  Measured medians,
-# split vs f32 kernel (profiles/r6_gemm_fp_sweep.jsonl): 1024^3 81 vs 25 us,
-# 1536^3 113 vs 79, 2048^3 (= 2^33) 153 vs 143, 4000x3000x1000 153 vs 230,
-# 3072^3 426 vs 604, 4096^3 696 vs 1088.  BEE_GEMM_F32X6: auto | 1 (whenever
-# the shape allows) | 0 (never).
+# split vs f32 kernel (profiles/r6_gemm_fp_sweep.jsonl, f32 kernel with the
+# buffer loads): 1024^3 81 vs 26 us, 1536^3 113 vs 80, 2048^3 (= 2^33) 153
+# vs 138, 4000x3000x1000 153 vs 191, 3072^3 426 vs 424 (level), 4096^3 696
+# vs 1005.  BEE_GEMM_F32X6: auto | 1 (whenever the shape allows) | 0 (never).
 _F32X6 = os.environ.get("BEE_GEMM_F32X6", "auto")
 _F32X6_MIN_MACS = (1 << 33) + 1
 

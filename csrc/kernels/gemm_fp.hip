@@ -15,15 +15,17 @@
 // the LDS and L2, so the design goal is simply to keep every SIMD issuing
 // MFMAs back to back:
 //
-//  * workgroup tile 128x128, 4 waves of 64x64; each wave holds 4x4
-//    accumulators of 16x16 (f64: 128 VGPRs, f32: 64), so one k-step of 4
-//    needs 4 A + 4 B one-element fragment reads for 16 MFMAs (1024 / 512
-//    cycles of MFMA per 8 ds_read);
-//  * K tile of 128 bytes per row (16 f64 / 32 f32): 16 KiB per operand, two
-//    LDS stages per operand = 72 KiB, so two workgroups share a CU and one's
-//    barrier hides behind the other's MFMAs;
-//  * global -> registers -> LDS, two K tiles ahead, one barrier per K tile:
-//    a tile's 16-B loads are in flight during a whole tile of MFMAs;
+//  * workgroup tile 64 x 64 (64 x 32 for mid-size products), 4 waves of
+//    32 x 32 (2 x 2 accumulators of 16x16) per K group; a k-step of 4 is 2 A
+//    + 2 B one-element fragment reads for 4 MFMAs, and the next k-step's
+//    reads are issued before this one's MFMAs (fragment lookahead);
+//  * K tile 16 deep (128 B per f64 row, 64 B per f32 row), two LDS stages,
+//    one barrier per K tile; global -> registers -> LDS through two register
+//    stages, so three K tiles of 16-B loads are in flight;
+//  * the loads go through one buffer descriptor per operand panel: rows and
+//    K columns past the matrix read as zero in hardware, so edge tiles, the
+//    partial K tile and the loop's tail run the same branch-free code as the
+//    interior (the f64 kernel needs 106 VGPRs, four workgroups per CU);
 //  * LDS holds each operand tile in its global orientation (rows copied as
 //    16-B chunks), padded so the fragment reads are bank-conflict free in
 //    either orientation -- so A^T / B^T views (numpy's a.T, e.g. np.dot(a.T,
@@ -32,32 +34,30 @@
 //    contiguous run of tiles, walked in groups of 8 tile rows (the A row
 //    panels and B column panels a group shares stay in that XCD's L2).
 //
-// Small products (fewer 128 x 64 tiles than half the chip's workgroup slots)
-// take 64-row tiles and, while still at most half full, two K groups per
-// workgroup whose halves meet in LDS (deterministic, no C memset;
-// profiles/archive/r5_gemm_fp_bm64.jsonl, r5_gemm_fp_splitk.jsonl).
+// Small products (at most ~1.5 64 x 64 tiles per CU) run two K groups per
+// workgroup whose halves meet in LDS (deterministic, no C memset).  128-row
+// tiles remain for A/B runs only (profiles/r6_gemm_fp_pmc.md).
 //
-// Any M, N, K and leading dimensions: out-of-range elements load as zero and
-// stores are masked; 16-B loads where pointers and leading dimensions allow,
-// element loads otherwise.
+// Any M, N, K and leading dimensions: 16-B buffer loads when the pointers,
+// leading dimensions and K allow them; otherwise guarded 16-B / element loads
+// (out-of-range elements zero).  Stores are masked.
 #include "bk_common.hpp"
 
 namespace bk {
 namespace fp {
 
-constexpr int kBM = 128, kBN = 128, kThreads = 256;
-constexpr int kPitchMN = 128 + 16;  // LDS row of an [k][m|n] tile: 144 elements
+constexpr int kBM = 128, kThreads = 256;  // (kBM: the A/B runs' 128-row tiles)
 
-// K tile: 128 B per row by default (16 f64 / 32 f32); an [m|n][k] LDS row is
-// padded by 16 B.  (Padding f32 rows by 8 B instead -- conflict-free for the
-// ds_read_b32 banking, (a/4) mod 32 -- and keeping every fragment read a
-// single ds_read_b32 / _b64 rather than the compiler's ds_read2 pairs measured
-// slower everywhere: 2048^3 f32 164 vs 143 us, f64 303 vs 277; the pairs
-// halve the LDS instructions and their address arithmetic.)
+// An [m|n][k] LDS row is padded by 2 elements: 16 B for f64, 8 B for f32
+// (with 16 B the f32 fragment reads' ds_read2_b32 pairs put rows r and r + 8
+// on one bank; 8 B: bank conflicts / LDS-active 0.33 -> 0.14 at 2048^3 and
+// 0.5-1.5% faster at every size, profiles/r6_gemm_fp_sweep.jsonl "pad8").
+// (Splitting the pairs into single ds_read_b32 / _b64 reads measured slower
+// everywhere: 2048^3 f32 164 vs 143 us, f64 303 vs 277; the pairs halve the
+// LDS instructions and their address arithmetic.)
 template <typename T>
 struct Cfg {
-  static constexpr int kDefaultBK = 128 / sizeof(T);
-  static constexpr int pitch_k(int bk) { return bk + 16 / (int)sizeof(T); }
+  static constexpr int pitch_k(int bk) { return bk + 2; }
 };
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -175,9 +175,8 @@ struct Tile {
 };
 
 // C[M][N] = A . B, A[m][k] at a[TA ? k*lda + m : m*lda + k], B[k][n] at
-// b[TB ? n*ldb + k : k*ldb + n].  Workgroup tile BM x BN (128 x 128, 128 x
-// 64, or for small products 64 x 64 / 64 x 32); 4 waves of BM/2 x BN/2 per K
-// group.
+// b[TB ? n*ldb + k : k*ldb + n].  Workgroup tile BM x BN (64 x 64 / 64 x 32;
+// 128 x 64 / 128 x 128 for A/B runs); 4 waves of BM/2 x BN/2 per K group.
 //
 // KS = 2 (small products): two K groups of 4 waves each take one half of the
 // K tiles with their own LDS stages, and at the end group 1 hands its
@@ -486,28 +485,6 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
   }
 }
 
-// 128 x 64 tiles when they fill the chip's workgroup slots (occ per CU)
-// better than 128 x 128 ones: a grid of t tiles runs in ceil(t / slots)
-// rounds, and a last round that is mostly empty idles the CUs for a whole
-// tile's time.  4000 x 3000 f64 at 2 per CU: 768 square tiles = 1.5 rounds
-// (0.75 of the slots busy) vs 1504 narrow ones = 2.94 (0.98): 66% -> 74% of
-// torch.matmul (profiles/archive/r5_gemm_fp_bench.jsonl, r5_gemm_fp_tiles.jsonl).
-inline double round_fill(int64_t tiles, int64_t slots) {
-  const int64_t rounds = (tiles + slots - 1) / slots;
-  return rounds > 0 ? (double)tiles / (double)(rounds * slots) : 1.0;
-}
-inline bool narrow_tiles(int M, int N, int occ) {
-  if (N <= 64) return false;
-  const int64_t tm = (M + kBM - 1) / kBM, t128 = tm * ((N + 127) / 128);
-  if (t128 < 2 * kNumCU) return true;
-  // the round model holds at two per CU; at three (f32) a short last round
-  // runs its workgroups faster, and narrow tiles lost: 4096^3 f32 0.84 vs
-  // 0.88 of torch.matmul with square ones (gpurun_out r5 bench 6 vs 4)
-  if (occ > 2) return false;
-  const int64_t slots = (int64_t)occ * kNumCU;
-  return round_fill(tm * ((N + 63) / 64), slots) > round_fill(t128, slots) + 0.05;
-}
-
 struct LaunchArgs {
   const void *A, *B;
   void* C;
@@ -522,7 +499,7 @@ struct LaunchArgs {
 
 template <typename T, bool TA, bool TB, bool V, int BM, int BN, int BK, int OCC, int KS, int RS, bool PIPE>
 void go(const LaunchArgs& g) {
-  if constexpr (V) {
+  if constexpr (V && KS == 1) {
     if (g.buf) {
       gemm_fp_kernel<T, TA, TB, true, BM, BN, BK, OCC, KS, RS, PIPE, true><<<g.grid, kThreads * KS, 0, g.stream>>>(
           (const T*)g.A, (const T*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, g.gate, g.su, g.ss);
@@ -573,33 +550,25 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
     return v ? atoi(v) : dflt;
   };
   // f32: a 64-byte K tile (16 deep) halves the LDS a workgroup holds, so a
-  // CU keeps three of them resident (its registers allow it) instead of two
+  // CU keeps more of them resident
   const int bk = env("BK_GEMM_FP_BK", 16) == 32 ? 32 : 16;
-  const int occ = !kF64 && bk == 16 ? 3 : 2;
   const int nk = (K + bk - 1) / bk;
-  // 64-row tiles while the 128-row ones would leave the CUs short of work:
+  // 64-row tiles (profiles/r6_gemm_fp_pmc.md, "Tile shapes with the buffer
+  // loads": the 128-row tiles lost at every size once the buffer-load kernels
+  // let a CU hold four 64 x 64 f64 workgroups, eight f32 ones -- f32 3072^3
+  // 423 vs 578 us with 128 x 128):
   //  * at most ~1.5 64 x 64 tiles per CU: two K groups per workgroup
   //    (1024^3: 256 tiles; f64 47 vs 51 us with one group);
-  //  * fewer 64 x 64 tiles than the chip's ~3 slots per CU: 64 x 32 tiles
-  //    (1536^3: f64 151 vs 165 us, f32 84 vs 86);
-  //  * f64 everywhere else (its 64 x 64 kernel runs three workgroups per
-  //    CU: 3072^3 856 vs 933 us, 4096^3 2001 vs 2126 with 128 x 128 tiles,
-  //    8192^3 15952 vs 16661); f32 while 128 x 64 tiles would not give
-  //    every CU two.
+  //  * fewer 64 x 64 tiles than ~3 per CU: 64 x 32 tiles (1536^3: f64 143
+  //    vs 166 us, f32 82 vs 87);
+  //  * 64 x 64 everywhere else.
   const int64_t t64 = (int64_t)((M + 63) / 64) * ((N + 63) / 64);
   const int64_t slots = 3 * (int64_t)kNumCU;
-  Shape s{kBM, 128, 1, 2};
-  if (2 * t64 <= slots && nk >= 16) {
+  Shape s{64, 64, 1, 2};
+  if (2 * t64 <= slots && nk >= 16)
     s = {64, 64, 2, 2};
-  } else if (t64 < slots) {
+  else if (t64 < slots)
     s = {64, 32, 1, 2};
-  } else if (kF64) {
-    s = {64, 64, 1, 2};
-  } else {
-    const bool nar = narrow_tiles(M, N, occ);
-    const bool small = nar && ((M + kBM - 1) / kBM) * (int64_t)((N + 63) / 64) < 2 * kNumCU;
-    s = {small ? 64 : kBM, nar ? 64 : 128, 1, 2};
-  }
   s.bm = env("BK_GEMM_FP_BM", s.bm) == 64 ? 64 : kBM;
   s.bn = env("BK_GEMM_FP_BN", s.bn);
   if (s.bn != 32 && s.bn != 64) s.bn = 128;
@@ -610,10 +579,12 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   const int64_t tiles = (int64_t)((M + s.bm - 1) / s.bm) * ((N + s.bn - 1) / s.bn);
   // BUF (branch-free buffer loads, the guarded path compiled out) when the
   // 16-B chunks along K are all in or all out (K a multiple of the chunk)
-  // and every panel offset -- rows up to a tile past the edge -- fits 31 bits
+  // and every panel offset -- rows up to a tile past the edge -- fits 31 bits;
+  // not for two K groups (one workgroup per CU there, so the registers it
+  // frees buy nothing: 1024^3 f64 50.3 vs 48.1 us, f32 27.6 vs 26.6)
   constexpr int kE = 16 / (int)sizeof(T);
   auto fits = [](int64_t rows, int64_t ld) { return (rows + 256) * ld * (int64_t)sizeof(T) < 0x7fffffffll; };
-  const bool buf = vec && K % kE == 0 && env("BK_GEMM_FP_BUF", 1) != 0 &&
+  const bool buf = vec && K % kE == 0 && s.ks == 1 && env("BK_GEMM_FP_BUF", 1) != 0 &&
                    fits(TA ? K : s.bm, lda) && fits(TB ? s.bn : K, ldb);
   LaunchArgs g{A, B, C, M, N, K, lda, ldb, ldc, stream, gate, env("BK_GEMM_FP_SU", 0), env("BK_GEMM_FP_SS", 1),
                (unsigned)tiles, buf};
