@@ -46,6 +46,15 @@
 namespace bk {
 namespace fp {
 
+// The MFMA step of a K tile (0-3) before which the next tile is staged (its
+// LDS stores, then the global loads that refill its registers): 2 -- the
+// LDS writes and the loads issue mid-tile, between MFMAs, not in one burst
+// with the tile's first fragment reads; 1.6% faster (geometric mean over f64
+// / f32 1536-4096^3) than 0, 1 level (profiles/r6_gemm_fp_sweep.jsonl,
+// session r6_s29).  A -D for A/B builds.
+#ifndef BK_FP_STORE_AT
+#define BK_FP_STORE_AT 2
+#endif
 constexpr int kBM = 128, kThreads = 256;  // (kBM: the A/B runs' 128-row tiles)
 
 // An [m|n][k] LDS row is padded by 2 elements: 16 B for f64, 8 B for f32
@@ -304,10 +313,11 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
   auto lds_b = [&](int st) { return stage0 + st * kStage + TileA::kLdsElems; };
 
   // Pipeline (two LDS stages, RS register stages, loads 1 + RS K tiles
-  // ahead): iteration kt first stores tile kt+1 -- in registers since
-  // iteration kt-RS -- into the other LDS stage (last read in iteration
-  // kt-1, before the barrier that ended it), then issues tile kt+1+RS's
-  // global loads into the freed registers, then runs tile kt's MFMAs.
+  // ahead): iteration kt stores tile kt+1 -- in registers since iteration
+  // kt-RS -- into the other LDS stage (last read in iteration kt-1, before
+  // the barrier that ended it), then issues tile kt+1+RS's global loads into
+  // the freed registers, while it runs tile kt's MFMAs (before step
+  // BK_FP_STORE_AT; the edge-tile variant at the top of the iteration).
   const int nk_all = (K + BK - 1) / BK, nk_per = (nk_all + KS - 1) / KS;
   const int kt0 = grp * nk_per;                      // this group's K tiles: [kt0, kt0 + nk)
   const int nk = max(0, min(nk_per, nk_all - kt0));  // (group 1 may have one fewer, or none)
@@ -365,13 +375,17 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
     constexpr int q = decltype(slot)::value;
     constexpr bool kFast = decltype(fast_tag)::value;
     const int cur = kt & 1;
-    if constexpr (kFast) {
+    auto stage_next = [&]() {
       ta[q].store(lds_a(cur ^ 1), tid);
       tb[q].store(lds_b(cur ^ 1), tid);
       if constexpr (BUF)
         load(slot, kpos(kt + 1 + RS));  // (past the end: zero tiles)
       else
         load_fast(slot, kpos(min(kt + 1 + RS, nk - 1)));
+    };
+    constexpr int kStoreAt = PIPE ? BK_FP_STORE_AT : 0;
+    if constexpr (kFast) {
+      if constexpr (kStoreAt == 0) stage_next();
     } else {
       if (kt >= nk) {  // (group 1's surplus iteration: only the barrier)
         __syncthreads();
@@ -388,6 +402,8 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
     if constexpr (PIPE) {
 #pragma unroll
       for (int s4 = 0; s4 < kSteps; ++s4) {
+        if constexpr (kFast && kStoreAt > 0)
+          if (s4 == kStoreAt) stage_next();
         T ca[MI], cb[NT];
 #pragma unroll
         for (int i = 0; i < MI; ++i) ca[i] = pa[i];
