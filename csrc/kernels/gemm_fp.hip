@@ -371,7 +371,7 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
   // flight together -- with the guarded, branchy loads the compiler's wait
   // before each LDS store drains every slot (vmcnt(0)).
   const bool fast = BUF || ((PIPE || RS > 1) && interior && nk == nk_per && (!partial || nk >= 2));
-  auto step = [&](int kt, auto slot, auto fast_tag) {  // slot = (kt + 1) % RS
+  auto step = [&](int kt, auto slot, auto fast_tag) __attribute__((always_inline)) {  // slot = (kt + 1) % RS
     constexpr int q = decltype(slot)::value;
     constexpr bool kFast = decltype(fast_tag)::value;
     const int cur = kt & 1;
@@ -441,11 +441,20 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
   };
   // (both variants run nk_per iterations: the K groups meet at every barrier)
   auto run = [&](auto fast_tag) {
-    for (int kt = 0; kt < nk_per; kt += RS) {
+    // (the loop body runs both register slots' steps unconditionally and an
+    // odd last step follows it: with the second step conditional inside the
+    // loop, the path that skipped it reached the first step's LDS stores with
+    // one slot of loads in flight, and the compiler's wait there drained both
+    // slots on every path -- vmcnt(0) every other K tile.  1024^3 / 1536^3
+    // 1-2.5% faster, larger sizes level: profiles/r6_gemm_fp_sweep.jsonl,
+    // session r6_s30)
+    int kt = 0;
+    for (; kt + RS <= nk_per; kt += RS) {
       step(kt, std::integral_constant<int, 1 % RS>{}, fast_tag);
-      if constexpr (RS > 1)
-        if (kt + 1 < nk_per) step(kt + 1, S0{}, fast_tag);
+      if constexpr (RS > 1) step(kt + 1, S0{}, fast_tag);
     }
+    if constexpr (RS > 1)
+      if (kt < nk_per) step(kt, std::integral_constant<int, 1 % RS>{}, fast_tag);
   };
   // (BUF: one branch-free loop for every tile; the guarded variant and its
   // registers are not in the kernel at all -- f64 64 x 64: 110 VGPRs
