@@ -574,9 +574,14 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
     const char* v = getenv(name);
     return v ? atoi(v) : dflt;
   };
-  // f32: a 64-byte K tile (16 deep) halves the LDS a workgroup holds, so a
-  // CU keeps more of them resident
-  const int bk = env("BK_GEMM_FP_BK", 16) == 32 ? 32 : 16;
+  const int64_t t64 = (int64_t)((M + 63) / 64) * ((N + 63) / 64);
+  const int64_t slots = 3 * (int64_t)kNumCU;
+  // K tile 16 deep; f32 products of fewer 64 x 64 tiles than ~3 per CU 32
+  // deep (each workgroup then has a CU to itself and halves its barriers:
+  // 1024^3 25.2 vs 26.0 us, 1536^3 75.3 vs 76.4; larger ones keep the
+  // 64-byte tile, whose halved LDS lets a CU hold more workgroups --
+  // profiles/r6_gemm_fp_sweep.jsonl, session r6_s32)
+  const int bk = env("BK_GEMM_FP_BK", !kF64 && t64 < slots ? 32 : 16) == 32 ? 32 : 16;
   const int nk = (K + bk - 1) / bk;
   // 64-row tiles (profiles/r6_gemm_fp_pmc.md, "Tile shapes with the buffer
   // loads": the 128-row tiles lost at every size once the buffer-load kernels
@@ -587,8 +592,6 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   //  * fewer 64 x 64 tiles than ~3 per CU: 64 x 32 tiles (1536^3: f64 143
   //    vs 166 us, f32 82 vs 87);
   //  * 64 x 64 everywhere else.
-  const int64_t t64 = (int64_t)((M + 63) / 64) * ((N + 63) / 64);
-  const int64_t slots = 3 * (int64_t)kNumCU;
   Shape s{64, 64, 1, 2};
   if (2 * t64 <= slots && nk >= 16)
     s = {64, 64, 2, 2};
