@@ -105,6 +105,30 @@ def test_gemm_fp_ragged_and_padded(gpu, dtype, M, N, K, lda, ldb, ldc):
     assert isinstance(c, DeviceArray)
 
 
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+def test_gemm_fp_wide_leading_dimension_past_31_bit_offsets(gpu, dtype):
+    """Rows 256 MiB apart, so row 8 of A starts 2 GiB into the buffer: the
+    buffer-descriptor loads (32-bit offsets) must not take the product -- the
+    launcher falls back to the guarded loads (gemm_fp.hip, fits()) -- and
+    every row still lands in C (a wrapped offset would read another row)."""
+    from bee_code_interpreter_fs_amd.ops import _native
+    from bee_code_interpreter_fs_amd.ops.array import driver
+
+    M, N, K = 9, 40, 64
+    lda = (1 << 28) // np.dtype(dtype).itemsize
+    rng = np.random.default_rng(17)
+    A = np.zeros((M, lda), dtype=dtype)  # (2.25 GiB; untouched pages stay unmapped on the host)
+    A[:, :K] = rng.standard_normal((M, K))
+    a_k = A[:, :K].astype(np.float64)
+    B = rng.standard_normal((K, N)).astype(dtype)
+    a, b = gpu.asarray(A), gpu.asarray(B)
+    del A
+    c = gpu.asarray(np.zeros((M, N), dtype=dtype))
+    driver().gemm_fp(_native.DTYPE_CODES[dtype], False, False, a.ptr, b.ptr, c.ptr, M, N, K, lda, N, N)
+    _check(c.numpy(), a_k, B.astype(np.float64), dtype)
+    del a
+
+
 def test_gemm_fp_propagates_nan_and_inf(gpu):
     a_h = np.ones((128, 64))
     b_h = np.ones((64, 128))
