@@ -576,26 +576,30 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   };
   const int64_t t64 = (int64_t)((M + 63) / 64) * ((N + 63) / 64);
   const int64_t slots = 3 * (int64_t)kNumCU;
-  // K tile 16 deep; f32 products of fewer 64 x 64 tiles than ~3 per CU 32
-  // deep (each workgroup then has a CU to itself and halves its barriers:
-  // 1024^3 25.2 vs 26.0 us, 1536^3 75.3 vs 76.4; larger ones keep the
-  // 64-byte tile, whose halved LDS lets a CU hold more workgroups --
-  // profiles/r6_gemm_fp_sweep.jsonl, session r6_s32)
-  const int bk = env("BK_GEMM_FP_BK", !kF64 && t64 < slots ? 32 : 16) == 32 ? 32 : 16;
-  const int nk = (K + bk - 1) / bk;
   // 64-row tiles (profiles/r6_gemm_fp_pmc.md, "Tile shapes with the buffer
   // loads": the 128-row tiles lost at every size once the buffer-load kernels
   // let a CU hold four 64 x 64 f64 workgroups, eight f32 ones -- f32 3072^3
   // 423 vs 578 us with 128 x 128):
   //  * at most ~1.5 64 x 64 tiles per CU: two K groups per workgroup
   //    (1024^3: 256 tiles; f64 47 vs 51 us with one group);
-  //  * fewer 64 x 64 tiles than ~3 per CU: 64 x 32 tiles (1536^3: f64 143
-  //    vs 166 us, f32 82 vs 87);
+  //  * 64 x 32 tiles where they share the work out over the CUs clearly more
+  //    evenly: `fill` is the busy share of the CUs when every CU takes
+  //    ceil(tiles / CUs) tiles, and a 64 x 32 tile does less work per loaded
+  //    byte, so it must gain > 0.1 of it (1536^3 0.90 vs 0.75: f64 143 vs
+  //    166 us; 1792^3 0.875 vs 0.77: 211 vs 223; 1280^3 0.78 both: 64 x 64,
+  //    92 vs 99; 2560^3 0.96 vs 0.89: 64 x 64, 530 vs 548 --
+  //    profiles/r6_gemm_fp_sweep.jsonl, sessions r6_s24, r6_s35);
   //  * 64 x 64 everywhere else.
+  auto fill = [](int64_t n) {
+    const int64_t per = (n + kNumCU - 1) / kNumCU;
+    return per > 0 ? (double)n / (double)(per * kNumCU) : 1.0;
+  };
+  // (f32: two K groups come with the 32-deep K tile below, so they need K >= 512)
+  const int nk_split = kF64 ? (K + 15) / 16 : (K + 31) / 32;
   Shape s{64, 64, 1, 2};
-  if (2 * t64 <= slots && nk >= 16)
+  if (2 * t64 <= slots && nk_split >= 16)
     s = {64, 64, 2, 2};
-  else if (t64 < slots)
+  else if (fill(2 * t64) > fill(t64) + 0.1)
     s = {64, 32, 1, 2};
   s.bm = env("BK_GEMM_FP_BM", s.bm) == 64 ? 64 : kBM;
   s.bn = env("BK_GEMM_FP_BN", s.bn);
@@ -604,6 +608,12 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   if (s.bm == kBM && s.bn == 32) s.bn = 64;  // (and 128-row ones 64 or 128)
   s.ks = s.bm == 64 && s.bn == 64 && env("BK_GEMM_FP_KS", s.ks) == 2 ? 2 : 1;
   s.rs = env("BK_GEMM_FP_RS", s.rs) == 1 ? 1 : 2;
+  // K tile 16 deep; f32 32 deep on the small products' shapes -- two K
+  // groups or 64 x 32 tiles -- where it halves the barriers (1024^3 25.2 vs
+  // 26.0 us, 1536^3 75.3 vs 76.4), 16 on 64 x 64 tiles, whose halved LDS
+  // lets a CU hold more workgroups (1280^3 51.3 vs 52.5; sessions r6_s32,
+  // r6_s35)
+  const int bk = env("BK_GEMM_FP_BK", !kF64 && (s.ks == 2 || s.bn == 32) ? 32 : 16) == 32 ? 32 : 16;
   const int64_t tiles = (int64_t)((M + s.bm - 1) / s.bm) * ((N + s.bn - 1) / s.bn);
   // BUF (branch-free buffer loads, the guarded path compiled out) when the
   // 16-B chunks along K are all in or all out (K a multiple of the chunk)
