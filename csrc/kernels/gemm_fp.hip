@@ -457,7 +457,7 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
       if (kt < nk_per) step(kt, std::integral_constant<int, 1 % RS>{}, fast_tag);
   };
   // (BUF: one branch-free loop for every tile; the guarded variant and its
-  // registers are not in the kernel at all -- f64 64 x 64: 110 VGPRs
+  // registers are not in the kernel at all -- f64 64 x 64: 112 VGPRs
   // against 152, a fourth workgroup per CU)
   if constexpr (BUF) {
     run(std::true_type{});
@@ -524,7 +524,7 @@ struct LaunchArgs {
 
 template <typename T, bool TA, bool TB, bool V, int BM, int BN, int BK, int OCC, int KS, int RS, bool PIPE>
 void go(const LaunchArgs& g) {
-  if constexpr (V && KS == 1) {
+  if constexpr (V) {
     if (g.buf) {
       gemm_fp_kernel<T, TA, TB, true, BM, BN, BK, OCC, KS, RS, PIPE, true><<<g.grid, kThreads * KS, 0, g.stream>>>(
           (const T*)g.A, (const T*)g.B, (T*)g.C, g.M, g.N, g.K, g.lda, g.ldb, g.ldc, g.gate, g.su, g.ss);
@@ -617,12 +617,13 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   const int64_t tiles = (int64_t)((M + s.bm - 1) / s.bm) * ((N + s.bn - 1) / s.bn);
   // BUF (branch-free buffer loads, the guarded path compiled out) when the
   // 16-B chunks along K are all in or all out (K a multiple of the chunk)
-  // and every panel offset -- rows up to a tile past the edge -- fits 31 bits;
-  // not for two K groups (one workgroup per CU there, so the registers it
-  // frees buy nothing: 1024^3 f64 50.3 vs 48.1 us, f32 27.6 vs 26.6)
+  // and every panel offset -- rows up to a tile past the edge -- fits 31 bits
+  // (two K groups too since the register-slot loop keeps a slot in flight:
+  // f32 1024^3 23.6 vs 24.2 us, 768^3 18.2 vs 18.8, f64 level; before it
+  // they were slower, 50.3 vs 48.1 -- sessions r6_s23, r6_s37)
   constexpr int kE = 16 / (int)sizeof(T);
   auto fits = [](int64_t rows, int64_t ld) { return (rows + 256) * ld * (int64_t)sizeof(T) < 0x7fffffffll; };
-  const bool buf = vec && K % kE == 0 && s.ks == 1 && env("BK_GEMM_FP_BUF", 1) != 0 &&
+  const bool buf = vec && K % kE == 0 && env("BK_GEMM_FP_BUF", 1) != 0 &&
                    fits(TA ? K : s.bm, lda) && fits(TB ? s.bn : K, ldb);
   LaunchArgs g{A, B, C, M, N, K, lda, ldb, ldc, stream, gate, env("BK_GEMM_FP_SU", 0), env("BK_GEMM_FP_SS", 1),
                (unsigned)tiles, buf};
