@@ -547,7 +547,9 @@ template <typename T, bool TA, bool TB, bool V, int BK, int OCC>
 void by_shape(const LaunchArgs& g, const Shape& s) {
   constexpr bool kF64 = std::is_same<T, double>::value;
   if (s.bm == 64) {
-    if (s.bn == 32)
+    if (s.bn == 32 && s.ks == 2)
+      go<T, TA, TB, V, 64, 32, BK, OCC, 2, 2, true>(g);
+    else if (s.bn == 32)
       s.rs == 2 ? go<T, TA, TB, V, 64, 32, BK, OCC, 1, 2, true>(g) : go<T, TA, TB, V, 64, 32, BK, OCC, 1, 1, true>(g);
     else if (s.ks == 2)
       s.rs == 2 ? go<T, TA, TB, V, 64, 64, BK, OCC, 2, 2, true>(g) : go<T, TA, TB, V, 64, 64, BK, OCC, 2, 1, true>(g);
@@ -565,7 +567,9 @@ void by_shape(const LaunchArgs& g, const Shape& s) {
 // (tools/gemm_fp_bench.py, tools/gemm_fp_sweep.sh) the choice can be
 // overridden: BK_GEMM_FP_BN (32 | 64 | 128 columns), BK_GEMM_FP_BM (64 | 128
 // rows), BK_GEMM_FP_KS (1 | 2 K groups), BK_GEMM_FP_RS (1 | 2 register
-// stages), BK_GEMM_FP_BK (f32: 16 | 32 deep), BK_GEMM_FP_SU / _SS (stagger).
+// stages), BK_GEMM_FP_BK (f32: 16 | 32 deep), BK_GEMM_FP_SU / _SS (stagger),
+// BK_GEMM_FP_TINY=0 (no 64 x 32 split for the smallest grids),
+// BK_GEMM_FP_BUF=0 (guarded loads only).
 template <typename T, bool TA, bool TB>
 void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, bool vec,
             hipStream_t stream, const unsigned* gate = nullptr) {
@@ -580,6 +584,10 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   // loads": the 128-row tiles lost at every size once the buffer-load kernels
   // let a CU hold four 64 x 64 f64 workgroups, eight f32 ones -- f32 3072^3
   // 423 vs 578 us with 128 x 128):
+  //  * at most half a 64 x 64 tile per CU: 64 x 32 tiles with two K groups,
+  //    twice the workgroups of the 64 x 64 split (f64 512^3 13.5 vs 21.2 us,
+  //    640^3 16.4 vs 25.2; f32 512^3 9.3 vs 13.3 -- session r6_s38; from
+  //    768^3 it lost, r6_s34);
   //  * at most ~1.5 64 x 64 tiles per CU: two K groups per workgroup
   //    (1024^3: 256 tiles; f64 47 vs 51 us with one group);
   //  * 64 x 32 tiles where they share the work out over the CUs clearly more
@@ -597,7 +605,9 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   // (f32: two K groups come with the 32-deep K tile below, so they need K >= 512)
   const int nk_split = kF64 ? (K + 15) / 16 : (K + 31) / 32;
   Shape s{64, 64, 1, 2};
-  if (2 * t64 <= slots && nk_split >= 16)
+  if (2 * t64 <= kNumCU && nk_split >= 16 && env("BK_GEMM_FP_TINY", 1) != 0)
+    s = {64, 32, 2, 2};
+  else if (2 * t64 <= slots && nk_split >= 16)
     s = {64, 64, 2, 2};
   else if (fill(2 * t64) > fill(t64) + 0.1)
     s = {64, 32, 1, 2};
@@ -606,7 +616,7 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   if (s.bn != 32 && s.bn != 64) s.bn = 128;
   if (s.bm == 64 && s.bn == 128) s.bn = 64;  // (64-row tiles come 64 or 32 wide)
   if (s.bm == kBM && s.bn == 32) s.bn = 64;  // (and 128-row ones 64 or 128)
-  s.ks = s.bm == 64 && s.bn == 64 && env("BK_GEMM_FP_KS", s.ks) == 2 ? 2 : 1;
+  s.ks = s.bm == 64 && s.bn <= 64 && env("BK_GEMM_FP_KS", s.ks) == 2 ? 2 : 1;
   s.rs = env("BK_GEMM_FP_RS", s.rs) == 1 ? 1 : 2;
   // K tile 16 deep; f32 32 deep on the small products' shapes -- two K
   // groups or 64 x 32 tiles -- where it halves the barriers (1024^3 25.2 vs
