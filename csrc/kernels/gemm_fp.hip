@@ -46,14 +46,18 @@
 namespace bk {
 namespace fp {
 
-// The MFMA step of a K tile (0-3) before which the next tile is staged (its
-// LDS stores, then the global loads that refill its registers): 2 -- the
-// LDS writes and the loads issue mid-tile, between MFMAs, not in one burst
-// with the tile's first fragment reads; 1.6% faster (geometric mean over f64
-// / f32 1536-4096^3) than 0, 1 level (profiles/r6_gemm_fp_sweep.jsonl,
-// session r6_s29).  A -D for A/B builds.
+// The MFMA steps of a K tile (0-3) before which the next tile is staged:
+// its LDS stores before step 1, the global loads that refill its registers
+// before step 2 -- mid-tile, between MFMAs, not in one burst with the tile's
+// first fragment reads.  Both at step 2 was 1.6% faster (geometric mean over
+// f64 / f32 1536-4096^3) than both at the top (session r6_s29); splitting
+// them 1 / 2 another 0.8% (2 / 3 0.5%, 1 / 3 level: session r6_s39;
+// profiles/r6_gemm_fp_sweep.jsonl).  -D for A/B builds.
 #ifndef BK_FP_STORE_AT
-#define BK_FP_STORE_AT 2
+#define BK_FP_STORE_AT 1
+#endif
+#ifndef BK_FP_LOAD_AT  // (the refill loads' step, >= BK_FP_STORE_AT)
+#define BK_FP_LOAD_AT 2
 #endif
 constexpr int kBM = 128, kThreads = 256;  // (kBM: the A/B runs' 128-row tiles)
 
@@ -316,8 +320,9 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
   // ahead): iteration kt stores tile kt+1 -- in registers since iteration
   // kt-RS -- into the other LDS stage (last read in iteration kt-1, before
   // the barrier that ended it), then issues tile kt+1+RS's global loads into
-  // the freed registers, while it runs tile kt's MFMAs (before step
-  // BK_FP_STORE_AT; the edge-tile variant at the top of the iteration).
+  // the freed registers, while it runs tile kt's MFMAs (before steps
+  // BK_FP_STORE_AT / BK_FP_LOAD_AT; the edge-tile variant at the top of the
+  // iteration).
   const int nk_all = (K + BK - 1) / BK, nk_per = (nk_all + KS - 1) / KS;
   const int kt0 = grp * nk_per;                      // this group's K tiles: [kt0, kt0 + nk)
   const int nk = max(0, min(nk_per, nk_all - kt0));  // (group 1 may have one fewer, or none)
@@ -375,17 +380,22 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
     constexpr int q = decltype(slot)::value;
     constexpr bool kFast = decltype(fast_tag)::value;
     const int cur = kt & 1;
-    auto stage_next = [&]() {
+    auto store_next = [&]() {
       ta[q].store(lds_a(cur ^ 1), tid);
       tb[q].store(lds_b(cur ^ 1), tid);
+    };
+    auto load_next = [&]() {
       if constexpr (BUF)
         load(slot, kpos(kt + 1 + RS));  // (past the end: zero tiles)
       else
         load_fast(slot, kpos(min(kt + 1 + RS, nk - 1)));
     };
     constexpr int kStoreAt = PIPE ? BK_FP_STORE_AT : 0;
+    constexpr int kLoadAt = PIPE ? BK_FP_LOAD_AT : 0;
+    static_assert(kLoadAt >= kStoreAt, "a slot's loads follow its LDS stores");
     if constexpr (kFast) {
-      if constexpr (kStoreAt == 0) stage_next();
+      if constexpr (kStoreAt == 0) store_next();
+      if constexpr (kLoadAt == 0) load_next();
     } else {
       if (kt >= nk) {  // (group 1's surplus iteration: only the barrier)
         __syncthreads();
@@ -403,7 +413,9 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
 #pragma unroll
       for (int s4 = 0; s4 < kSteps; ++s4) {
         if constexpr (kFast && kStoreAt > 0)
-          if (s4 == kStoreAt) stage_next();
+          if (s4 == kStoreAt) store_next();
+        if constexpr (kFast && kLoadAt > 0)
+          if (s4 == kLoadAt) load_next();
         T ca[MI], cb[NT];
 #pragma unroll
         for (int i = 0; i < MI; ++i) ca[i] = pa[i];
