@@ -591,7 +591,6 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
     return v ? atoi(v) : dflt;
   };
   const int64_t t64 = (int64_t)((M + 63) / 64) * ((N + 63) / 64);
-  const int64_t slots = 3 * (int64_t)kNumCU;
   // 64-row tiles (profiles/r6_gemm_fp_pmc.md, "Tile shapes with the buffer
   // loads": the 128-row tiles lost at every size once the buffer-load kernels
   // let a CU hold four 64 x 64 f64 workgroups, eight f32 ones -- f32 3072^3
@@ -600,8 +599,10 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   //    twice the workgroups of the 64 x 64 split (f64 512^3 13.5 vs 21.2 us,
   //    640^3 16.4 vs 25.2; f32 512^3 9.3 vs 13.3 -- session r6_s38; from
   //    768^3 it lost, r6_s34);
-  //  * at most ~1.5 64 x 64 tiles per CU: two K groups per workgroup
-  //    (1024^3: 256 tiles; f64 47 vs 51 us with one group);
+  //  * at most one 64 x 64 tile per CU: two K groups per workgroup (1024^3:
+  //    256 tiles; f64 47 vs 51 us with one group; past one per CU a second
+  //    round of these 8-wave workgroups lost to 64 x 32 tiles, 1152^3 79.3
+  //    vs 65.2 us -- session r6_s41);
   //  * 64 x 32 tiles where they share the work out over the CUs clearly more
   //    evenly: `fill` is the busy share of the CUs when every CU takes
   //    ceil(tiles / CUs) tiles, and a 64 x 32 tile does less work per loaded
@@ -619,7 +620,7 @@ void launch(const void* A, const void* B, void* C, int M, int N, int K, int64_t 
   Shape s{64, 64, 1, 2};
   if (2 * t64 <= kNumCU && nk_split >= 16 && env("BK_GEMM_FP_TINY", 1) != 0)
     s = {64, 32, 2, 2};
-  else if (2 * t64 <= slots && nk_split >= 16)
+  else if (t64 <= kNumCU && nk_split >= 16)
     s = {64, 64, 2, 2};
   else if (fill(2 * t64) > fill(t64) + 0.1)
     s = {64, 32, 1, 2};
