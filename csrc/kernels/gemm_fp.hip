@@ -277,9 +277,15 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
   // rows ([k][n]) or its rows n0.. ([n][k]) -- whose range ends at the
   // matrix's last element, so rows past M / N / K read as zero
   // (launch() checks every panel offset fits 31 bits)
+  // (num_records is 32 bits: a panel of 2 GiB or more -- the rest of a big
+  // matrix from this tile's first row -- is capped at 2^31 - 1, which every
+  // in-range offset stays below (launch()'s fits()); cast unclamped, 4 GiB
+  // and up would wrap to a short range and read real rows as zero)
   auto panel = [](const T* base, int64_t elems) {
     const int64_t bytes = elems * (int64_t)sizeof(T);
-    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(bytes < 0 ? 0 : bytes), 0x00020000);
+    const int64_t cap = 0x7fffffffll;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(bytes < 0 ? 0 : bytes > cap ? cap : bytes),
+                                             0x00020000);
   };
   const __amdgpu_buffer_rsrc_t ra =
       TA ? panel(a + m0, (int64_t)(K - 1) * lda + M - m0) : panel(a + (int64_t)m0 * lda, (int64_t)(M - m0 - 1) * lda + K);

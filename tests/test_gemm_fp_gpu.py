@@ -129,6 +129,29 @@ def test_gemm_fp_wide_leading_dimension_past_31_bit_offsets(gpu, dtype):
     del a
 
 
+def test_gemm_fp_buffer_loads_on_a_matrix_past_4_gib(gpu):
+    """A 4.5 GB f64 operand whose 64-row panels still have 31-bit offsets
+    (lda 800000 elements, so the buffer-descriptor loads take it): the
+    descriptor's 32-bit range must be capped, not wrapped -- wrapped, the
+    range from the first tile's row would end 28 rows in, and the rows past
+    it would read as zero."""
+    from bee_code_interpreter_fs_amd.ops import _native
+    from bee_code_interpreter_fs_amd.ops.array import driver
+
+    M, N, K, lda = 700, 64, 64, 800_000
+    rng = np.random.default_rng(19)
+    A = np.zeros((M, lda))  # (4.5 GB; untouched pages stay unmapped on the host)
+    A[:, :K] = rng.standard_normal((M, K))
+    a_k = A[:, :K].copy()
+    B = rng.standard_normal((K, N))
+    a, b = gpu.asarray(A), gpu.asarray(B)
+    del A
+    c = gpu.asarray(np.zeros((M, N)))
+    driver().gemm_fp(_native.DTYPE_CODES["float64"], False, False, a.ptr, b.ptr, c.ptr, M, N, K, lda, N, N)
+    _check(c.numpy(), a_k, B, "float64")
+    del a
+
+
 def test_gemm_fp_propagates_nan_and_inf(gpu):
     a_h = np.ones((128, 64))
     b_h = np.ones((64, 128))
