@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 6, session 44: the final tree (buffer range cap) -- the whole GPU
+# suite, smoke, the driver's bench.
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+source tools/gpu_steps.sh
+export TMPDIR=/tmp
+step r6_gputests 1100 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step r6_smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step r6_bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5
