@@ -31,7 +31,7 @@
 //    either orientation -- so A^T / B^T views (numpy's a.T, e.g. np.dot(a.T,
 //    a)) are read in place, no transpose pass;
 //  * XCD-aware tile order: blocks land on XCD b % 8, so each XCD gets a
-//    contiguous run of tiles, walked in groups of 8 tile rows (the A row
+//    contiguous run of tiles, walked in groups of 4 tile rows (the A row
 //    panels and B column panels a group shares stay in that XCD's L2).
 //
 // Small products (at most ~1.5 64 x 64 tiles per CU) run two K groups per
@@ -58,6 +58,13 @@ namespace fp {
 #endif
 #ifndef BK_FP_LOAD_AT  // (the refill loads' step, >= BK_FP_STORE_AT)
 #define BK_FP_LOAD_AT 2
+#endif
+// The tile order walks groups of this many tile rows (their A panels, and
+// the B panels the group shares, stay in the XCD's L2): 4 -- 0.8% faster than
+// 8 over f64 / f32 2048-8192^3 (f64 8192^3 15730 vs 16262 us), 16 2% slower
+// (session r6_s45).  -D for A/B builds.
+#ifndef BK_FP_GROUP
+#define BK_FP_GROUP 4
 #endif
 constexpr int kBM = 128, kThreads = 256;  // (kBM: the A/B runs' 128-row tiles)
 
@@ -239,7 +246,7 @@ __global__ __launch_bounds__(kThreads * KS, OCC) void gemm_fp_kernel(const T* __
   // total % 8 XCDs one more), whose A / B panels then share that XCD's L2
   const int per_xcd = total / kNumXCD, extra = total % kNumXCD, xcd = raw % kNumXCD;
   const int bid = xcd * per_xcd + min(xcd, extra) + raw / kNumXCD;
-  constexpr int kGroup = 8;
+  constexpr int kGroup = BK_FP_GROUP;  // tile rows walked together (their A panels shared in L2)
   const int per_group = kGroup * tiles_n;
   const int first_m = (bid / per_group) * kGroup;
   const int gsz = min(tiles_m - first_m, kGroup);
