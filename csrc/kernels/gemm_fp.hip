@@ -61,8 +61,8 @@ namespace fp {
 #endif
 // The tile order walks groups of this many tile rows (their A panels, and
 // the B panels the group shares, stay in the XCD's L2): 4 -- 0.8% faster than
-// 8 over f64 / f32 2048-8192^3 (f64 8192^3 15730 vs 16262 us), 16 2% slower
-// (session r6_s45).  -D for A/B builds.
+// 8 over f64 / f32 2048-8192^3 (f64 8192^3 15730 vs 16262 us), 16 2% slower,
+// 2 1.75% slower, 1 4.5% (sessions r6_s45, r6_s47).  -D for A/B builds.
 #ifndef BK_FP_GROUP
 #define BK_FP_GROUP 4
 #endif
